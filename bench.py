@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark: complex Msamples/s through the 255-tap FIR on MI355X.
+
+Workload (BASELINE.json configs[1]): 255-tap real-tap FIR, decimate by 4, over complex
+f32 IQ (nominal 2.4 Msps stream -> 600 ksps), single channel per GPU, 2^28 input samples
+per step, inputs resident in HBM.  One step = one sdrgpu_fir_process_dev() call over the
+whole batch (the FIR state carries across steps, as a stream would).
+
+Multi-GPU (torchrun, one process per GPU): each rank filters its own time shard of the
+stream (weak scaling; no data-path collective -- SURVEY.md 8e).  Timing: barrier +
+synchronize on both sides of exactly K steps, MAX over ranks; value = all ranks' samples
+/ that time.
+
+Also reported (rank 0, N=1 only unless --cpu-baseline force):
+  roofline      algorithmic bytes per launch (10 B / input sample) / the
+                kernel's average HIP-event-timed duration, vs 8 TB/s HBM3E;
+  cpu_baseline  the oracle (C restatement of Fir::apply + Decimate, 1 core) on a bounded
+                sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "unnamed-rust-sdr_amd"))
+
+METRIC = "complex Msamples/sec through 255-tap FIR, 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3
+BYTES_PER_SAMPLE = 8 + 8 / 4   # c64 in + c64 out at decim 4
+FLOPS_PER_SAMPLE = 255 * 4 / 4 # direct form, kept outputs only
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2n", type=int, default=28, help="input samples per GPU per step")
+    ap.add_argument("--algo", default="auto", choices=["auto", "direct", "os"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_fir_c2.json"))
+    return ap.parse_args()
+
+
+def synth_iq(torch, n, seed, device):
+    """x = sum of 3 tones (random f in +-0.4 fs, amp 0.3) + 0.1 N(0,1), complex (8d)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    x = torch.randn(n, 2, device=device, generator=g) * 0.1
+    t = torch.arange(n, device=device, dtype=torch.float64)
+    r = np.random.default_rng(seed)
+    for f in r.uniform(-0.4, 0.4, 3):
+        ph = torch.remainder(t * float(f), 1.0) * (2 * np.pi)
+        x[:, 0] += (0.3 * torch.cos(ph)).float()
+        x[:, 1] += (0.3 * torch.sin(ph)).float()
+        del ph
+    del t
+    return x.reshape(-1).contiguous()
+
+
+def cpu_baseline(taps, seconds):
+    """Oracle (restated reference path: all outputs computed, 3 of 4 dropped) on 1 core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    rng = np.random.default_rng(1)
+    chunk = 1 << 18
+    x = ((rng.standard_normal(chunk) + 1j * rng.standard_normal(chunk)) * 0.3).astype(np.complex64)
+    f = pyoracle.Fir(taps, 4, sample_kind=1)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        f.process(x)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el / 1e6, "unit": "complex Msamples/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{done} c64 samples ({done // chunk} blocks of 2^18) through the oracle "
+                      f"Fir(255 taps)+Decimate(4), {el:.1f} s on 1 host core"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu import _lib
+
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    n = 1 << args.log2n
+    D = 4
+    algo = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE}[args.algo]
+    fir = sdrgpu.filter.Fir(taps, decim=D, sample_kind=_lib.C64, device=local,
+                            algorithm=algo).design(2.4e6)
+    stream = torch.cuda.current_stream(dev)
+    fir.set_stream(stream.cuda_stream)
+
+    x = synth_iq(torch, n, seed=1000 + rank, device=dev)  # this rank's time shard
+    n_out = n // D
+    y = torch.empty(2 * n_out, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        got = fir.process_dev(x.data_ptr(), n, y.data_ptr(), n_out)
+        assert got == n_out, (got, n_out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    total_samples = n * args.steps * world
+    value = total_samples / elapsed / 1e6
+    if rank == 0:
+        achieved = BYTES_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                pm = json.load(open(args.pmc_json))
+                if pm.get("log2n") == args.log2n and pm.get("algo", "auto") == args.algo:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "complex Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (3 tones + noise, complex64, on-device)",
+            "config": {
+                "workload": "configs[1]: 255-tap FIR (real f32 taps, firwin 0.2) decimate-by-4 "
+                            "on complex IQ, single channel per GPU",
+                "samples_per_gpu_per_step": n,
+                "ntaps": 255, "decim": D, "sample": "c64", "taps": "f32",
+                "algorithm": args.algo,
+                "parallelism": f"{world} time shards, no data-path collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kern_ms, 4),
+                "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * n),
+                "fp32_tflops_direct_equiv": round(FLOPS_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e12, 2),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(taps, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

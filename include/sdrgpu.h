@@ -1,0 +1,207 @@
+/*
+ * sdrgpu.h -- C ABI of the MI355X-native sample-stream core (FIR / FIR-decimate,
+ * framed FFT / STFT, batched PLL) that replaces the CPU hot path of the Rust crate
+ * agrif/unnamed-rust-sdr (`sdr` 0.1.0).
+ *
+ * Every entry point names the reference interface it replaces (path:line in the
+ * reference tree).  The ABI is modelled on the crate's only existing FFI boundary,
+ * src/resample.rs (libsamplerate-sys):
+ *   - opaque handle per filter, create/clone/reset/destroy
+ *     (SampleRate::new / try_clone / reset / Drop, src/resample.rs:32-110);
+ *   - int error codes, 0 = OK, positive = named error, sdrgpu_strerror()
+ *     (resample::Error, src/resample.rs:151-270);
+ *   - block-oriented process() (SampleRate::process, src/resample.rs:46-67) -- a
+ *     per-sample FFI call would be infeasible, so the Rust side buffers samples.
+ *
+ * Threading: a handle is Send, not Sync (the Block adapter moves filters across rayon
+ * workers, src/signal/adapters/block.rs:142-146).  Calls on one handle must not run
+ * concurrently; a handle may migrate between threads.  Each handle owns one HIP stream
+ * (or uses one set with *_set_stream).
+ *
+ * Buffers: the plain functions take HOST pointers and are synchronous.  The *_dev
+ * variants take DEVICE pointers (on the handle's device), enqueue on the handle's stream
+ * and return immediately; call *_sync or synchronise the stream before reading.
+ *
+ * Sample layout: SDRGPU_F32 = float; SDRGPU_C64 = {float re, im} interleaved, i.e.
+ * num::Complex<f32> (#[repr(C)]).  Sizes are counted in SAMPLES, not bytes.
+ */
+#ifndef SDRGPU_H
+#define SDRGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDRGPU_ABI_VERSION 1
+
+/* ---- error codes (style of resample::Error, src/resample.rs:151-270) ---- */
+enum sdrgpu_status {
+    SDRGPU_OK = 0,
+    SDRGPU_ERR_INVALID = 1,      /* null handle/pointer, zero taps, zero decimation, bad kind */
+    SDRGPU_ERR_NOMEM = 2,        /* host or device allocation failed */
+    SDRGPU_ERR_DEVICE = 3,       /* HIP runtime error (copy, stream, sync) */
+    SDRGPU_ERR_NODEVICE = 4,     /* no GPU, or device index out of range */
+    SDRGPU_ERR_UNSUPPORTED = 5,  /* valid request this build does not implement */
+    SDRGPU_ERR_OUTPUT_CAP = 6,   /* output capacity smaller than the samples produced */
+    SDRGPU_ERR_LAUNCH = 7,       /* kernel launch failed */
+};
+
+enum sdrgpu_kind {
+    SDRGPU_F32 = 0,  /* f32 */
+    SDRGPU_C64 = 1,  /* num::Complex<f32> */
+};
+
+/* FIR algorithm selection (results agree within the parity tolerance). */
+enum sdrgpu_fir_algo {
+    SDRGPU_FIR_AUTO = 0,          /* pick per shape */
+    SDRGPU_FIR_DIRECT = 1,        /* LDS-tiled direct form, register-blocked outputs */
+    SDRGPU_FIR_OVERLAP_SAVE = 2,  /* polyphase overlap-save, LDS-resident FFT tiles */
+};
+
+const char* sdrgpu_strerror(int code);   /* resample::Error Display, src/resample.rs:209-269 */
+int sdrgpu_abi_version(void);
+int sdrgpu_device_count(int* count);
+
+/* =====================================================================================
+ * FIR / FIR-decimate.
+ * Replaces: Fir::new / Fir::apply            (src/filter/fir.rs:12-32)
+ *           Convolve::accumulate (MAC)       (src/filter/convolve.rs:8-15)
+ *           FilterDesign for Fir/Vec<C>/&[C] (src/filter/fir.rs:36-58)
+ *           Signal::filter + adapters::Filter::next (src/signal/mod.rs:42-48,
+ *                                            src/signal/adapters/mod.rs:77-96)
+ *           Signal::decimate + Decimate::next (src/signal/mod.rs:26-28,
+ *                                            src/signal/adapters/mod.rs:19-37)
+ * y[n] = sum_{k<ntaps} taps[k] * x[n-k], x[<0] = 0 (zero history, fir.rs:15); with
+ * decim D > 1 only outputs at stream indices D-1, 2D-1, ... are produced (the reference
+ * computes all and Decimate drops D-1 of every D; only the kept ones are computed here).
+ * State (ntaps-1 history, decimation phase) carries across process() calls, so any
+ * partition of a stream into blocks gives the same outputs.
+ * Kinds: (F32,F32), (C64,F32), (C64,C64).  (F32 samples with C64 taps do not type-check
+ * in the reference: f32 is not Mul<Complex<f32>, Output=f32>.)
+ * ===================================================================================== */
+typedef struct sdrgpu_fir sdrgpu_fir;
+
+int sdrgpu_fir_create(int device, int sample_kind, int tap_kind, const void* taps,
+                      size_t ntaps, uint32_t decim, sdrgpu_fir** out);
+int sdrgpu_fir_set_algorithm(sdrgpu_fir* h, int algo);
+/* Use an external hipStream_t (NULL restores the handle's own stream). */
+int sdrgpu_fir_set_stream(sdrgpu_fir* h, void* hip_stream);
+/* Number of outputs the next process() call produces for n_in inputs. */
+int sdrgpu_fir_output_len(const sdrgpu_fir* h, size_t n_in, size_t* n_out);
+int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
+                       size_t out_cap, size_t* n_out);
+int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d_out,
+                           size_t out_cap, size_t* n_out);
+int sdrgpu_fir_sync(sdrgpu_fir* h);
+int sdrgpu_fir_reset(sdrgpu_fir* h);                           /* FilterDesign::design -> fresh state */
+int sdrgpu_fir_clone(const sdrgpu_fir* h, sdrgpu_fir** out);   /* #[derive(Clone)] Fir, fir.rs:6 */
+void sdrgpu_fir_destroy(sdrgpu_fir* h);
+
+/* Batched FIR bank: nch independent channels sharing one tap set, per-channel state.
+ * Channel c's samples start at in + c*ld_in (ld in samples).  Same semantics per
+ * channel as sdrgpu_fir (each channel is one Fir, src/filter/fir.rs:6-32). */
+typedef struct sdrgpu_firbank sdrgpu_firbank;
+
+int sdrgpu_firbank_create(int device, int sample_kind, int tap_kind, const void* taps,
+                          size_t ntaps, uint32_t decim, size_t nch, sdrgpu_firbank** out);
+int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo);
+int sdrgpu_firbank_set_stream(sdrgpu_firbank* h, void* hip_stream);
+int sdrgpu_firbank_output_len(const sdrgpu_firbank* h, size_t n_in, size_t* n_out);
+int sdrgpu_firbank_process(sdrgpu_firbank* h, const void* in, size_t ld_in, size_t n_in,
+                           void* out, size_t ld_out, size_t* n_out);
+int sdrgpu_firbank_process_dev(sdrgpu_firbank* h, const void* d_in, size_t ld_in,
+                               size_t n_in, void* d_out, size_t ld_out, size_t* n_out);
+int sdrgpu_firbank_sync(sdrgpu_firbank* h);
+int sdrgpu_firbank_reset(sdrgpu_firbank* h);
+int sdrgpu_firbank_clone(const sdrgpu_firbank* h, sdrgpu_firbank** out);
+void sdrgpu_firbank_destroy(sdrgpu_firbank* h);
+
+/* =====================================================================================
+ * FFT.
+ * Replaces: fft::fft  (src/fft.rs:3-28)  -- forward DFT, fftshift collate, x 1/sqrt(N)
+ *           fft::rfft (src/fft.rs:30-37)  -- real input, keeps output bins [N/2, N)
+ * exec transforms `count` back-to-back frames of n C64 samples; out[i] of each frame is
+ * X[(i - n/2) mod n] / sqrt(n) (fft.rs:14-26).  Frequencies (fft.rs:18,24) are
+ * (i - n/2) * rate / n and are produced host-side by sdrgpu_fft_freqs.
+ * n must be a power of two, 2 <= n <= 2^20 (rustfft accepts any n: other sizes return
+ * SDRGPU_ERR_UNSUPPORTED).
+ * ===================================================================================== */
+typedef struct sdrgpu_fft sdrgpu_fft;
+
+int sdrgpu_fft_plan(int device, size_t n, sdrgpu_fft** out);
+int sdrgpu_fft_set_stream(sdrgpu_fft* h, void* hip_stream);
+int sdrgpu_fft_exec(sdrgpu_fft* h, const void* in, void* out, size_t count);
+int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t count);
+/* rfft: `count` frames of n F32 samples -> count frames of n/2 C64 bins [n/2, n). */
+int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count);
+int sdrgpu_fft_sync(sdrgpu_fft* h);
+void sdrgpu_fft_destroy(sdrgpu_fft* h);
+int sdrgpu_fft_freqs(size_t n, float rate, float* freqs);
+
+/* STFT = sig.window(n/rate).decimate(rate/hop).map(fft::fft)  (examples/live.rs:29-39):
+ * Window keeps the last n samples zero-prefilled (src/signal/adapters/mod.rs:277-299);
+ * Decimate(wait=hop) yields a frame after every hop-th input (adapters/mod.rs:30-37).
+ * Frame j covers stream samples [(j+1)hop - n, (j+1)hop).  Streaming: state carries
+ * across calls. */
+typedef struct sdrgpu_stft sdrgpu_stft;
+
+int sdrgpu_stft_create(int device, size_t n, size_t hop, sdrgpu_stft** out);
+int sdrgpu_stft_set_stream(sdrgpu_stft* h, void* hip_stream);
+int sdrgpu_stft_output_len(const sdrgpu_stft* h, size_t n_in, size_t* n_frames);
+int sdrgpu_stft_process(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
+                        size_t out_cap_frames, size_t* n_frames);
+int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void* d_out,
+                            size_t out_cap_frames, size_t* n_frames);
+int sdrgpu_stft_sync(sdrgpu_stft* h);
+int sdrgpu_stft_reset(sdrgpu_stft* h);
+void sdrgpu_stft_destroy(sdrgpu_stft* h);
+
+/* =====================================================================================
+ * Biquad designs and batched PLL.
+ * Replaces: BiquadD::design (src/filter/biquad.rs:73-155), Biquad::new/apply (:25-56),
+ *           filter::Identity (src/filter/simple.rs:3-19),
+ *           PllDesign::new/design (src/filter/pll.rs:25-60), Pll::apply (:70-85).
+ * One PLL per channel; output[i] = Some(output) -> value, None -> 0.0 (src/main.rs:49
+ * unwrap_or(0.0)), locked[i] = 1 when Some.
+ * ===================================================================================== */
+enum sdrgpu_biquad_kind {
+    SDRGPU_BQ_IDENTITY = 0,
+    SDRGPU_BQ_LOWPASS = 1,   /* BiquadD::LowPass(freq, q)  */
+    SDRGPU_BQ_HIGHPASS = 2,  /* BiquadD::HighPass(freq, q) */
+    SDRGPU_BQ_BANDPASS = 3,  /* BiquadD::BandPass(freq, q) */
+    SDRGPU_BQ_NOTCH = 4,     /* BiquadD::Notch(freq, q)    */
+    SDRGPU_BQ_LR = 5,        /* BiquadD::Lr(decayrate) -- freq field, q ignored */
+};
+typedef struct { int32_t kind; float freq; float q; } sdrgpu_biquad_design;
+
+typedef struct {
+    float reference;                 /* PllDesign::new reference (Hz)  */
+    float gain;                      /* PllDesign::new gain            */
+    float rate;                      /* FilterDesign::design(rate)     */
+    sdrgpu_biquad_design loopf;      /* on Complex<f32>                */
+    sdrgpu_biquad_design outputf;    /* on f32                         */
+    sdrgpu_biquad_design lockf;      /* on f32                         */
+} sdrgpu_pll_params;
+
+typedef struct sdrgpu_pll sdrgpu_pll;
+
+int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu_pll** out);
+int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
+int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,
+                       float* out, uint8_t* locked, size_t ld_out);
+int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t n,
+                           float* d_out, uint8_t* d_locked, size_t ld_out);
+/* Public Pll fields nphase / value (src/filter/pll.rs:20-21) of channel ch. */
+int sdrgpu_pll_state(sdrgpu_pll* h, size_t ch, float* nphase, float* value_re_im);
+int sdrgpu_pll_sync(sdrgpu_pll* h);
+int sdrgpu_pll_reset(sdrgpu_pll* h);
+int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out);
+void sdrgpu_pll_destroy(sdrgpu_pll* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDRGPU_H */

@@ -1,0 +1,465 @@
+/*
+ * oracle.c -- CPU restatement of the agrif/unnamed-rust-sdr hot path (TEST ONLY).
+ * See oracle.h for the contract.  Build: oracle/Makefile (-O2 -ffp-contract=off).
+ * Every function cites the reference file:line it restates.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#if defined(__FLT_EVAL_METHOD__) && __FLT_EVAL_METHOD__ != 0
+#error "f32 arithmetic must evaluate in f32 (x86-64 SSE), as Rust does"
+#endif
+
+typedef struct { float re, im; } c32;
+
+/* num-complex 0.2 arithmetic, as used by Convolve::accumulate (convolve.rs:13-15):
+ *   Complex * f32      = (re*c, im*c)
+ *   Complex * Complex  = (a.re*b.re - a.im*b.im, a.re*b.im + a.im*b.re)
+ *   AddAssign          = component-wise += */
+static inline c32 cmul_r(c32 a, float c) { c32 r = {a.re * c, a.im * c}; return r; }
+static inline c32 cmul(c32 a, c32 b) {
+    c32 r;
+    r.re = a.re * b.re - a.im * b.im;
+    r.im = a.re * b.im + a.im * b.re;
+    return r;
+}
+
+/* ================================ FIR ================================= */
+struct oracle_fir {
+    int sk, tk;            /* sample / tap kind */
+    size_t K;
+    uint32_t D;
+    float* taps;           /* K (f32) or 2K (c64) */
+    float* ring;           /* 2K samples (doubled ring, newest at [head]) */
+    size_t head;
+    uint64_t seen;         /* samples consumed (decimation phase) */
+};
+
+oracle_fir* oracle_fir_create(int sk, int tk, const float* taps, size_t ntaps,
+                              uint32_t decim) {
+    if (ntaps == 0 || decim == 0) return NULL;
+    if (sk == ORACLE_F32 && tk == ORACLE_C64) return NULL; /* f32: !Mul<Complex> */
+    oracle_fir* f = (oracle_fir*)calloc(1, sizeof(*f));
+    f->sk = sk; f->tk = tk; f->K = ntaps; f->D = decim;
+    size_t tw = (tk == ORACLE_C64) ? 2 : 1, sw = (sk == ORACLE_C64) ? 2 : 1;
+    f->taps = (float*)malloc(sizeof(float) * tw * ntaps);
+    memcpy(f->taps, taps, sizeof(float) * tw * ntaps);
+    f->ring = (float*)calloc(2 * ntaps * sw, sizeof(float));
+    oracle_fir_reset(f);
+    return f;
+}
+
+void oracle_fir_destroy(oracle_fir* f) {
+    if (!f) return;
+    free(f->taps); free(f->ring); free(f);
+}
+
+/* Fir::new zero-fills the history (fir.rs:12-19). */
+void oracle_fir_reset(oracle_fir* f) {
+    size_t sw = (f->sk == ORACLE_C64) ? 2 : 1;
+    memset(f->ring, 0, sizeof(float) * 2 * f->K * sw);
+    f->head = 0;
+    f->seen = 0;
+}
+
+/* Fir::apply (fir.rs:23-32): pop_back, push_front(value), then
+ *   accum = 0; for (c, v) in coef.zip(buffer) { accum += v * c }
+ * buffer[0] is the newest sample.  The doubled ring keeps buffer[k] = ring[head+k]
+ * contiguous; arithmetic order is unchanged. */
+static inline void fir_push(oracle_fir* f, const float* x) {
+    size_t K = f->K;
+    f->head = (f->head == 0) ? K - 1 : f->head - 1;
+    if (f->sk == ORACLE_C64) {
+        f->ring[2 * f->head] = x[0]; f->ring[2 * f->head + 1] = x[1];
+        f->ring[2 * (f->head + K)] = x[0]; f->ring[2 * (f->head + K) + 1] = x[1];
+    } else {
+        f->ring[f->head] = x[0]; f->ring[f->head + K] = x[0];
+    }
+}
+
+static inline void fir_dot(const oracle_fir* f, float* y) {
+    size_t K = f->K;
+    if (f->sk == ORACLE_F32) {
+        const float* b = f->ring + f->head;
+        float acc = 0.0f;
+        for (size_t k = 0; k < K; ++k) acc += b[k] * f->taps[k];
+        y[0] = acc;
+    } else if (f->tk == ORACLE_F32) {
+        const c32* b = (const c32*)(f->ring) + f->head;
+        c32 acc = {0.0f, 0.0f};
+        for (size_t k = 0; k < K; ++k) {
+            c32 p = cmul_r(b[k], f->taps[k]);
+            acc.re += p.re; acc.im += p.im;
+        }
+        y[0] = acc.re; y[1] = acc.im;
+    } else {
+        const c32* b = (const c32*)(f->ring) + f->head;
+        const c32* h = (const c32*)f->taps;
+        c32 acc = {0.0f, 0.0f};
+        for (size_t k = 0; k < K; ++k) {
+            c32 p = cmul(b[k], h[k]);
+            acc.re += p.re; acc.im += p.im;
+        }
+        y[0] = acc.re; y[1] = acc.im;
+    }
+}
+
+/* Signal::filter(taps).decimate(rate) (signal/mod.rs:26-28,42-48; adapters/mod.rs:30-37):
+ * every input runs Fir::apply; Decimate keeps upstream indices wait-1, 2wait-1, ... */
+size_t oracle_fir_process(oracle_fir* f, const float* in, size_t n_in, float* out) {
+    size_t sw = (f->sk == ORACLE_C64) ? 2 : 1;
+    size_t n_out = 0;
+    float y[2];
+    for (size_t i = 0; i < n_in; ++i) {
+        fir_push(f, in + i * sw);
+        fir_dot(f, y);           /* the reference computes every output */
+        f->seen++;
+        if (f->seen % f->D == 0) {
+            memcpy(out + n_out * sw, y, sizeof(float) * sw);
+            n_out++;
+        }
+    }
+    return n_out;
+}
+
+typedef struct {
+    int sk, tk; const float* taps; size_t ntaps; uint32_t D;
+    const float* in; size_t ld_in; size_t n_in; float* out; size_t ld_out;
+    size_t ch0, ch1; size_t n_out;
+} fir_job;
+
+static void* fir_job_run(void* arg) {
+    fir_job* j = (fir_job*)arg;
+    size_t sw = (j->sk == ORACLE_C64) ? 2 : 1;
+    oracle_fir* f = oracle_fir_create(j->sk, j->tk, j->taps, j->ntaps, j->D);
+    for (size_t c = j->ch0; c < j->ch1; ++c) {
+        oracle_fir_reset(f);
+        j->n_out = oracle_fir_process(f, j->in + c * j->ld_in * sw, j->n_in,
+                                      j->out + c * j->ld_out * sw);
+    }
+    oracle_fir_destroy(f);
+    return NULL;
+}
+
+size_t oracle_fir_batch(int sk, int tk, const float* taps, size_t ntaps, uint32_t D,
+                        size_t nch, const float* in, size_t ld_in, size_t n_in,
+                        float* out, size_t ld_out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((size_t)nthreads > nch) nthreads = (int)(nch ? nch : 1);
+    pthread_t th[256];
+    fir_job jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; ++t) {
+        fir_job* j = &jobs[t];
+        j->sk = sk; j->tk = tk; j->taps = taps; j->ntaps = ntaps; j->D = D;
+        j->in = in; j->ld_in = ld_in; j->n_in = n_in; j->out = out; j->ld_out = ld_out;
+        j->ch0 = nch * t / nthreads; j->ch1 = nch * (t + 1) / nthreads; j->n_out = 0;
+        pthread_create(&th[t], NULL, fir_job_run, j);
+    }
+    size_t n_out = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].ch1 > jobs[t].ch0) n_out = jobs[t].n_out;
+    }
+    return n_out;
+}
+
+/* ================================ Biquad ================================ */
+/* BiquadD::design (biquad.rs:83-155) then Biquad::new (:25-38).  All f32. */
+static const float PI_F = 3.14159265358979323846f; /* std::f32::consts::PI */
+
+static void bq_new(float a0, float a1, float a2, float b0, float b1, float b2,
+                   oracle_biquad_coefs* c) {
+    c->b0 = b0 / a0;
+    c->b1 = b1 / a0;
+    c->b2 = b2 / a0;
+    c->na1 = -a1 / a0;
+    c->na2 = -a2 / a0;
+}
+
+void oracle_biquad_design_coefs(oracle_biquad_design d, float rate, oracle_biquad_coefs* c) {
+    float omega, cs, alpha;
+    switch (d.kind) {
+    case ORACLE_BQ_LOWPASS:   /* biquad.rs:89-101 */
+        omega = 2.0f * PI_F * d.freq / rate;
+        cs = cosf(omega);
+        alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, (1.0f - cs) / 2.0f, 1.0f - cs,
+               (1.0f - cs) / 2.0f, c);
+        break;
+    case ORACLE_BQ_HIGHPASS:  /* biquad.rs:102-114 */
+        omega = 2.0f * PI_F * d.freq / rate;
+        cs = cosf(omega);
+        alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, (1.0f + cs) / 2.0f, -1.0f - cs,
+               (1.0f + cs) / 2.0f, c);
+        break;
+    case ORACLE_BQ_BANDPASS:  /* biquad.rs:115-127 */
+        omega = 2.0f * PI_F * d.freq / rate;
+        cs = cosf(omega);
+        alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, alpha, 0.0f, -alpha, c);
+        break;
+    case ORACLE_BQ_NOTCH:     /* biquad.rs:128-140 */
+        omega = 2.0f * PI_F * d.freq / rate;
+        cs = cosf(omega);
+        alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, 1.0f, -2.0f * cs, 1.0f, c);
+        break;
+    case ORACLE_BQ_LR: {      /* biquad.rs:141-151 */
+        float decayn = d.freq / rate;
+        bq_new(1.0f, -expf(-decayn), 0.0f, decayn, 0.0f, 0.0f, c);
+        break;
+    }
+    default:                  /* Identity: y = x, represented as b0 = 1 */
+        c->b0 = 1.0f; c->b1 = 0.0f; c->b2 = 0.0f; c->na1 = 0.0f; c->na2 = 0.0f;
+        break;
+    }
+}
+
+typedef struct { oracle_biquad_coefs c; float x1, x2, y1, y2; int ident; } bq_r;
+typedef struct { oracle_biquad_coefs c; c32 x1, x2, y1, y2; } bq_c;
+
+/* Biquad::apply (biquad.rs:43-56): out = 0; out += v*b0; += x1*b1; += x2*b2;
+ * += y1*na1; += y2*na2; then x2 <- x1, x1 <- v, y2 <- y1, y1 <- out. */
+static inline float bq_r_apply(bq_r* s, float v) {
+    if (s->ident) return v;
+    float out = 0.0f;
+    out += v * s->c.b0;
+    out += s->x1 * s->c.b1;
+    out += s->x2 * s->c.b2;
+    out += s->y1 * s->c.na1;
+    out += s->y2 * s->c.na2;
+    s->x2 = s->x1; s->x1 = v;
+    s->y2 = s->y1; s->y1 = out;
+    return out;
+}
+
+static inline c32 bq_c_apply(bq_c* s, c32 v) {
+    c32 out = {0.0f, 0.0f}, p;
+    p = cmul_r(v, s->c.b0);     out.re += p.re; out.im += p.im;
+    p = cmul_r(s->x1, s->c.b1); out.re += p.re; out.im += p.im;
+    p = cmul_r(s->x2, s->c.b2); out.re += p.re; out.im += p.im;
+    p = cmul_r(s->y1, s->c.na1); out.re += p.re; out.im += p.im;
+    p = cmul_r(s->y2, s->c.na2); out.re += p.re; out.im += p.im;
+    s->x2 = s->x1; s->x1 = v;
+    s->y2 = s->y1; s->y1 = out;
+    return out;
+}
+
+void oracle_biquad_run(oracle_biquad_design d, float rate, int sk, const float* in,
+                       size_t n, float* out) {
+    if (sk == ORACLE_F32) {
+        bq_r s; memset(&s, 0, sizeof(s));
+        oracle_biquad_design_coefs(d, rate, &s.c);
+        s.ident = (d.kind == ORACLE_BQ_IDENTITY);
+        for (size_t i = 0; i < n; ++i) out[i] = bq_r_apply(&s, in[i]);
+    } else {
+        bq_c s; memset(&s, 0, sizeof(s));
+        oracle_biquad_design_coefs(d, rate, &s.c);
+        const c32* x = (const c32*)in; c32* y = (c32*)out;
+        if (d.kind == ORACLE_BQ_IDENTITY) { memcpy(out, in, n * sizeof(c32)); return; }
+        for (size_t i = 0; i < n; ++i) y[i] = bq_c_apply(&s, x[i]);
+    }
+}
+
+/* ================================ PLL ================================== */
+typedef struct {
+    float rate, reference, gain;
+    bq_c loopf; bq_r outf, lockf;
+    float nphase; c32 value;
+} pll_state;
+
+/* PllDesign::design (pll.rs:48-60) */
+static void pll_design(const oracle_pll_params* p, pll_state* s) {
+    memset(s, 0, sizeof(*s));
+    s->rate = p->rate;
+    s->reference = p->reference / p->rate;
+    s->gain = p->gain;
+    oracle_biquad_design_coefs(p->loopf, p->rate, &s->loopf.c);
+    oracle_biquad_design_coefs(p->outputf, p->rate, &s->outf.c);
+    s->outf.ident = (p->outputf.kind == ORACLE_BQ_IDENTITY);
+    oracle_biquad_design_coefs(p->lockf, p->rate, &s->lockf.c);
+    s->lockf.ident = (p->lockf.kind == ORACLE_BQ_IDENTITY);
+    s->nphase = 0.0f;
+    s->value.re = 0.0f; s->value.im = 0.0f;
+}
+
+/* Pll::apply (pll.rs:70-85). */
+static inline float pll_apply(pll_state* s, c32 x, uint8_t* locked_out, int loop_ident) {
+    c32 conjv = {s->value.re, -s->value.im};
+    c32 c = cmul(x, conjv);                                    /* :71 */
+    c32 lf = loop_ident ? c : bq_c_apply(&s->loopf, c);
+    float phasedif = atan2f(lf.im, lf.re) * s->gain;           /* :72 arg() */
+    s->nphase += s->reference + phasedif;                      /* :73 */
+    s->nphase = s->nphase - truncf(s->nphase);                 /* :74 fract() */
+    float phase = 2.0f * PI_F * s->nphase;                     /* :75 */
+    s->value.re = 1.0f * cosf(phase);                          /* :76 from_polar */
+    s->value.im = 1.0f * sinf(phase);
+    float locked = bq_r_apply(&s->lockf, c.re);                /* :78 */
+    float output = bq_r_apply(&s->outf, phasedif * s->rate);   /* :79 */
+    if (locked > 0.01f) { *locked_out = 1; return output; }    /* :80-84 */
+    *locked_out = 0;
+    return 0.0f;                                               /* main.rs:49 */
+}
+
+typedef struct {
+    const oracle_pll_params* p; const float* in; size_t ld_in, n; float* out;
+    uint8_t* locked; size_t ld_out; size_t ch0, ch1;
+} pll_job;
+
+static void* pll_job_run(void* arg) {
+    pll_job* j = (pll_job*)arg;
+    int loop_ident = (j->p->loopf.kind == ORACLE_BQ_IDENTITY);
+    for (size_t c = j->ch0; c < j->ch1; ++c) {
+        pll_state s; pll_design(j->p, &s);
+        const c32* x = (const c32*)j->in + c * j->ld_in;
+        float* y = j->out + c * j->ld_out;
+        uint8_t* lk = j->locked + c * j->ld_out;
+        for (size_t i = 0; i < j->n; ++i) y[i] = pll_apply(&s, x[i], &lk[i], loop_ident);
+    }
+    return NULL;
+}
+
+void oracle_pll_batch(const oracle_pll_params* p, size_t nch, const float* in,
+                      size_t ld_in, size_t n, float* out, uint8_t* locked,
+                      size_t ld_out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((size_t)nthreads > nch) nthreads = (int)(nch ? nch : 1);
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256]; pll_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        pll_job* j = &jobs[t];
+        j->p = p; j->in = in; j->ld_in = ld_in; j->n = n; j->out = out;
+        j->locked = locked; j->ld_out = ld_out;
+        j->ch0 = nch * t / nthreads; j->ch1 = nch * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, pll_job_run, j);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* ================================ FFT ================================== */
+typedef struct { double re, im; } c64d;
+
+static void dft_f64(c64d* a, size_t n) {
+    if (n == 0) return;
+    if ((n & (n - 1)) == 0) {
+        /* iterative radix-2 DIT, forward (sign -1) like rustfft FFTplanner::new(false) */
+        for (size_t i = 1, j = 0; i < n; ++i) {
+            size_t bit = n >> 1;
+            for (; j & bit; bit >>= 1) j ^= bit;
+            j ^= bit;
+            if (i < j) { c64d t = a[i]; a[i] = a[j]; a[j] = t; }
+        }
+        for (size_t len = 2; len <= n; len <<= 1) {
+            double ang = -2.0 * M_PI / (double)len;
+            for (size_t i = 0; i < n; i += len) {
+                for (size_t k = 0; k < len / 2; ++k) {
+                    double wr = cos(ang * (double)k), wi = sin(ang * (double)k);
+                    c64d u = a[i + k], v = a[i + k + len / 2];
+                    c64d t = {v.re * wr - v.im * wi, v.re * wi + v.im * wr};
+                    a[i + k].re = u.re + t.re; a[i + k].im = u.im + t.im;
+                    a[i + k + len / 2].re = u.re - t.re; a[i + k + len / 2].im = u.im - t.im;
+                }
+            }
+        }
+    } else {
+        c64d* t = (c64d*)malloc(sizeof(c64d) * n);
+        for (size_t k = 0; k < n; ++k) {
+            double sr = 0, si = 0;
+            for (size_t j = 0; j < n; ++j) {
+                double ang = -2.0 * M_PI * (double)((k * j) % n) / (double)n;
+                sr += a[j].re * cos(ang) - a[j].im * sin(ang);
+                si += a[j].re * sin(ang) + a[j].im * cos(ang);
+            }
+            t[k].re = sr; t[k].im = si;
+        }
+        memcpy(a, t, sizeof(c64d) * n);
+        free(t);
+    }
+}
+
+/* fft::fft collate (fft.rs:14-26): out[i] = X[(i - n/2) mod n] * (1/sqrt(n)) in f32. */
+void oracle_fft_frame(const float* in, size_t n, float* out) {
+    c64d* a = (c64d*)malloc(sizeof(c64d) * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) { a[i].re = in[2 * i]; a[i].im = in[2 * i + 1]; }
+    dft_f64(a, n);
+    float norm = 1.0f / sqrtf((float)n);
+    long start = -(long)(n / 2);
+    for (size_t i = 0; i < n; ++i) {
+        long srci = start + (long)i;
+        size_t pos = (size_t)(srci < 0 ? srci + (long)n : srci);
+        float re = (float)a[pos].re, im = (float)a[pos].im;
+        out[2 * i] = re * norm;
+        out[2 * i + 1] = im * norm;
+    }
+    free(a);
+}
+
+typedef struct {
+    const float* in; size_t n_in, n, hop; float* out; size_t f0, f1;
+} stft_job;
+
+static void* stft_job_run(void* arg) {
+    stft_job* j = (stft_job*)arg;
+    float* frame = (float*)malloc(sizeof(float) * 2 * j->n);
+    for (size_t f = j->f0; f < j->f1; ++f) {
+        long end = (long)((f + 1) * j->hop);          /* exclusive */
+        long beg = end - (long)j->n;
+        for (size_t i = 0; i < j->n; ++i) {
+            long g = beg + (long)i;
+            if (g < 0) { frame[2 * i] = 0.0f; frame[2 * i + 1] = 0.0f; }
+            else { frame[2 * i] = j->in[2 * g]; frame[2 * i + 1] = j->in[2 * g + 1]; }
+        }
+        oracle_fft_frame(frame, j->n, j->out + f * 2 * j->n);
+    }
+    free(frame);
+    return NULL;
+}
+
+/* Window::next keeps the last cap samples, zero-prefilled (adapters/mod.rs:277-299);
+ * Decimate(wait=hop) yields it after inputs hop-1, 2hop-1, ... (:30-37). */
+size_t oracle_stft(const float* in, size_t n_in, size_t n, size_t hop, float* out,
+                   size_t max_frames, int nthreads) {
+    size_t nf = n_in / hop;
+    if (nf > max_frames) nf = max_frames;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > nf) nthreads = (int)(nf ? nf : 1);
+    pthread_t th[256]; stft_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        stft_job* j = &jobs[t];
+        j->in = in; j->n_in = n_in; j->n = n; j->hop = hop; j->out = out;
+        j->f0 = nf * t / nthreads; j->f1 = nf * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, stft_job_run, j);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    return nf;
+}
+
+/* ================================ Sources =============================== */
+/* Freq -> FreqSweep::new(rate, f, 0, phase, 0, 0, None) (sources.rs:129-143,203-207)
+ * and FreqSweep::next (:150-175) with dfdt forced to 0. */
+void oracle_freq(float rate, float freq, float phase, size_t n, float* out) {
+    float dt = 1.0f / rate;
+    float f = freq;
+    float nphase = phase / (2.0f * PI_F);
+    for (size_t i = 0; i < n; ++i) {
+        float dfdt = 0.0f;
+        f += dt * dfdt;
+        nphase += dt * f;
+        nphase = nphase - truncf(nphase);
+        float ph = 2.0f * PI_F * nphase;
+        out[2 * i] = 1.0f * cosf(ph);
+        out[2 * i + 1] = 1.0f * sinf(ph);
+    }
+}
+
+/* RtlTcpSignal::next (rtltcp.rs:156-164): (v - 128) / 128 */
+void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
+    for (size_t i = 0; i < 2 * n; ++i) out[i] = ((float)in[i] - 128.0f) / 128.0f;
+}

@@ -1,0 +1,217 @@
+"""GPU parity tests: sdrgpu FIR / FIR-decimate / FIR bank (via the C ABI) vs the oracle.
+
+Reference semantics: Fir::apply (src/filter/fir.rs:23-32) + Decimate
+(src/signal/adapters/mod.rs:30-37).  Tolerance: 1e-5 of RMS.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, assert_parity, rms_rel_err
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def cplx(rng, n, dtype=np.complex64):
+    return (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(dtype)
+
+
+def make_case(rng, sk, tk, K, n):
+    taps = rng.standard_normal(K).astype(np.float32) / np.sqrt(K)
+    if tk == 1:
+        taps = (taps + 1j * rng.standard_normal(K) / np.sqrt(K)).astype(np.complex64)
+    x = cplx(rng, n) if sk == 1 else rng.standard_normal(n).astype(np.float32)
+    return taps, x
+
+
+ALGOS = ["direct", "auto"]
+
+
+def fir(sdr, taps, sk, D, algo="auto"):
+    from sdrgpu import _lib
+    a = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE}[algo]
+    return sdr.filter.Fir(taps, decim=D, sample_kind=sk, algorithm=a).design(2.4e6)
+
+
+CASES = [
+    # (sample_kind, tap_kind, ntaps, decim, n)
+    (1, 0, 255, 4, 10000),     # configs[1] shape
+    (0, 0, 127, 1, 5000),      # configs[0] shape
+    (1, 1, 63, 3, 3001),       # complex taps
+    (1, 0, 1, 1, 100),         # single tap (no history)
+    (1, 0, 5, 7, 33),          # D > K
+    (0, 0, 300, 2, 2000),
+    (1, 0, 255, 1, 70000),     # many workgroups
+    (1, 0, 255, 4, 1 << 18),
+    (1, 0, 2000, 16, 40000),   # long filter, heavy decimation
+    (1, 0, 33, 64, 50000),     # LDS fallback path (very large D)
+    (1, 1, 255, 4, 20000),
+    (0, 0, 64, 8, 9999),
+]
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "sk{}tk{}K{}D{}n{}".format(*c))
+def test_fir_parity(sdr, oracle, case, algo):
+    sk, tk, K, D, n = case
+    rng = np.random.default_rng(hash(case) % 2**32)
+    taps, x = make_case(rng, sk, tk, K, n)
+    ref = oracle.Fir(taps, D, sample_kind=sk).process(x)
+    y = fir(sdr, taps, sk, D, algo).process(x)
+    assert y.shape == ref.shape
+    assert_parity(y, ref, what=str(case))
+
+
+@pytest.mark.parametrize("name", ["fir_c1.npz", "fir_c2.npz", "fir_cc.npz"])
+def test_fir_golden(sdr, name):
+    g = np.load(os.path.join(GOLD, name), allow_pickle=False)
+    sk = int(np.iscomplexobj(g["x"]))
+    y = fir(sdr, g["taps"], sk, int(g["decim"])).process(g["x"])
+    assert_parity(y, g["y"], what=name)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_fir_block_partition_invariance(sdr, oracle, algo):
+    rng = np.random.default_rng(7)
+    taps, x = make_case(rng, 1, 0, 255, 50000)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(x)
+    whole = fir(sdr, taps, 1, 4, algo).process(x)
+    f = fir(sdr, taps, 1, 4, algo)
+    parts, i = [], 0
+    for step in (1, 2, 3, 5, 100, 253, 254, 255, 256, 4095, 1, 7777, 13, 20000):
+        parts.append(f.process(x[i:i + step]))
+        i += step
+    parts.append(f.process(x[i:]))
+    y = np.concatenate(parts)
+    assert_parity(y, ref, what="chunked")
+    if algo == "direct":
+        assert np.array_equal(y, whole)  # same per-output arithmetic, any partition
+
+
+def test_fir_empty_and_tiny_blocks(sdr, oracle):
+    rng = np.random.default_rng(3)
+    taps, x = make_case(rng, 1, 0, 255, 20)
+    f = fir(sdr, taps, 1, 4)
+    assert f.process(x[:0]).size == 0
+    o = oracle.Fir(taps, 4, sample_kind=1)
+    ys, rs = [], []
+    for i in range(20):  # one sample at a time, like Filter::apply
+        ys.append(f.process(x[i:i + 1]))
+        rs.append(o.process(x[i:i + 1]))
+        assert ys[-1].size == rs[-1].size
+    assert_parity(np.concatenate(ys), np.concatenate(rs))
+
+
+def test_fir_apply_single_sample_api(sdr, oracle):
+    taps = np.array([0.5, 0.25, 0.125], np.float32)
+    f = sdr.filter.Fir(taps, sample_kind=0).design(1.0)
+    o = oracle.Fir(taps, 1, sample_kind=0)
+    for v in [1.0, 0.0, 0.0, 2.0, -1.0]:
+        assert np.isclose(f.apply(v), o.process(np.array([v], np.float32))[0], atol=1e-7)
+    fd = sdr.filter.Fir(taps, decim=2, sample_kind=0).design(1.0)
+    assert fd.apply(1.0) is None and fd.apply(0.0) is not None
+
+
+def test_fir_output_cap_error(sdr):
+    import ctypes
+    from sdrgpu import _lib
+    taps = np.ones(8, np.float32)
+    f = fir(sdr, taps, 1, 1)
+    x = np.ones(100, np.complex64)
+    out = np.empty(10, np.complex64)
+    got = ctypes.c_size_t()
+    rc = _lib.lib().sdrgpu_fir_process(f._h, x.ctypes.data, 100, out.ctypes.data, 10,
+                                       ctypes.byref(got))
+    assert rc == _lib.ERR_OUTPUT_CAP and got.value == 100
+    # a rejected call leaves the state untouched
+    ref = np.convolve(x, taps)[:100]
+    assert_parity(f.process(x), ref)
+
+
+def test_fir_reset_and_clone(sdr, oracle):
+    rng = np.random.default_rng(11)
+    taps, x = make_case(rng, 1, 0, 255, 30000)
+    f = fir(sdr, taps, 1, 4)
+    a = f.process(x[:12345])
+    c = f.clone()  # #[derive(Clone)] snapshot of state (fir.rs:6)
+    b1 = f.process(x[12345:])
+    b2 = c.process(x[12345:])
+    assert np.array_equal(b1, b2)
+    f.reset()
+    assert np.array_equal(f.process(x[:12345]), a)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(x)
+    assert_parity(np.concatenate([a, b1]), ref)
+
+
+def test_firbank_parity(sdr, oracle):
+    rng = np.random.default_rng(5)
+    nch, n, K, D = 37, 5000, 255, 4
+    taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+    x = cplx(rng, nch * n).reshape(nch, n)
+    ref = oracle.fir_batch(taps, x, D, nthreads=8)
+    bank = sdr.filter.FirBank(taps, nch, sample_kind=1, decim=D)
+    y1 = bank.process(x[:, :1234])
+    y2 = bank.process(x[:, 1234:])
+    y = np.concatenate([y1, y2], axis=1)
+    assert y.shape == ref.shape
+    for c in range(nch):
+        assert_parity(y[c], ref[c], what=f"ch{c}")
+
+
+def test_fir_device_pointer_path_torch_stream(sdr, oracle):
+    import torch
+    rng = np.random.default_rng(9)
+    taps, x = make_case(rng, 1, 0, 255, 1 << 20)
+    f = fir(sdr, taps, 1, 4)
+    f.set_stream(torch.cuda.current_stream().cuda_stream)
+    dx = torch.from_numpy(x.view(np.float32)).cuda()
+    n_out = f.output_len(x.size)
+    dy = torch.empty(2 * n_out, dtype=torch.float32, device="cuda")
+    got = f.process_dev(dx.data_ptr(), x.size, dy.data_ptr(), n_out)
+    assert got == n_out
+    torch.cuda.synchronize()
+    y = dy.cpu().numpy().view(np.complex64)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(x)
+    assert_parity(y, ref)
+
+
+@pytest.mark.slow
+def test_fir_full_size_c2_properties(sdr, oracle):
+    """configs[1] at full size (2^28 c64): spot-check windows against the oracle (the FIR
+    is local: output m only depends on inputs g_m-254..g_m) and check linearity."""
+    import torch
+    n = 1 << 28
+    K, D = 255, 4
+    import scipy.signal as ss
+    taps = ss.firwin(K, 0.2).astype(np.float32)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    dx = torch.randn(2 * n, device="cuda", generator=g)
+    f = fir(sdr, taps, 1, D)
+    f.set_stream(torch.cuda.current_stream().cuda_stream)
+    n_out = n // D
+    dy = torch.empty(2 * n_out, dtype=torch.float32, device="cuda")
+    assert f.process_dev(dx.data_ptr(), n, dy.data_ptr(), n_out) == n_out
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0)
+    starts = [0, n_out - 4096] + list(rng.integers(1, n_out - 4096, 6))
+    for m0 in starts:
+        m0 = int(m0)
+        g0 = max(0, 4 * m0 - 256)          # covers the 254-sample reach of output m0
+        g1 = 4 * (m0 + 4096)
+        xin = dx[2 * g0:2 * g1].cpu().numpy().view(np.complex64)
+        ref = oracle.Fir(taps, D, sample_kind=1).process(xin)
+        skip = m0 - g0 // 4
+        ref = ref[skip:skip + 4096]
+        y = dy[2 * m0:2 * (m0 + 4096)].cpu().numpy().view(np.complex64)
+        assert_parity(y, ref, what=f"window {m0}")
+    # linearity over the whole 2^28 stream: F(2x) == 2 F(x) exactly (power-of-2 scale)
+    f2 = fir(sdr, taps, 1, D)
+    f2.set_stream(torch.cuda.current_stream().cuda_stream)
+    dy2 = torch.empty_like(dy)
+    dx.mul_(2.0)
+    f2.process_dev(dx.data_ptr(), n, dy2.data_ptr(), n_out)
+    torch.cuda.synchronize()
+    assert torch.equal(dy2, 2.0 * dy)

@@ -1,0 +1,389 @@
+// abi_fir.cpp -- C ABI of the streaming FIR / FIR-decimate and the FIR bank.
+//
+// Replaces Fir::new/apply + FilterDesign (reference src/filter/fir.rs:12-58) driven by
+// adapters::Filter (src/signal/adapters/mod.rs:77-96) and Decimate
+// (src/signal/adapters/mod.rs:19-37).  Stream state (K-1 history per channel, decimation
+// phase) is carried across calls so block partitioning never changes the outputs.
+#include <vector>
+
+#include "abi_common.hpp"
+#include "fir_kernels.hpp"
+
+using namespace sdrgpu;
+using namespace sdrgpu::detail;
+
+namespace sdrgpu {
+int fir_os_launch(const FirParams& p, void* os_state, hipStream_t s);
+void* fir_os_prepare(int device, int sample_kind, int tap_kind, const void* taps, int K,
+                     int D, hipStream_t s, int* status);
+void fir_os_release(void* os_state);
+}  // namespace sdrgpu
+
+struct FirCore {
+    int device = 0;
+    int sk = SDRGPU_C64, tk = SDRGPU_F32;
+    int K = 1, D = 1;
+    size_t nch = 1;
+    int algo = SDRGPU_FIR_AUTO;
+    std::vector<unsigned char> taps_host;  // original taps (for clone / OS prep)
+    int tpp = 0;
+    void* d_taps_pm = nullptr;
+    void* d_hist[2] = {nullptr, nullptr};  // ping-pong, nch x (K-1) samples each
+    int cur = 0;
+    unsigned long long seen = 0;           // stream samples consumed (decimation phase)
+    StreamSlot stream;
+    DevBuf stage_in, stage_out;
+    void* os_state = nullptr;              // overlap-save plan (lazily built)
+    int os_status = SDRGPU_OK;
+
+    size_t sbytes() const { return kind_bytes(sk); }
+    size_t hist_bytes() const { return nch * (size_t)(K - 1) * sbytes(); }
+
+    long first_kept() const {
+        const long g = (long)(seen % (unsigned long long)D);
+        return ((long)D - 1 - g) % D;
+    }
+    size_t out_len(size_t n_in) const {
+        const long i0 = first_kept();
+        return (long)n_in > i0 ? (size_t)(((long)n_in - 1 - i0) / D + 1) : 0;
+    }
+
+    void free_all() {
+        DeviceGuard g(device);
+        if (d_taps_pm) (void)hipFree(d_taps_pm);
+        for (auto& p : d_hist)
+            if (p) (void)hipFree(p);
+        d_taps_pm = nullptr;
+        d_hist[0] = d_hist[1] = nullptr;
+        stage_in.release();
+        stage_out.release();
+        if (os_state) fir_os_release(os_state);
+        os_state = nullptr;
+        stream.destroy();
+    }
+
+    int reset_state() {
+        DeviceGuard g(device);
+        if (!g.ok()) return SDRGPU_ERR_DEVICE;
+        seen = 0;
+        cur = 0;
+        if (K > 1) {
+            SDRGPU_HIP_TRY(hipMemsetAsync(d_hist[0], 0, hist_bytes(), stream.cur));
+            SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
+        }
+        return SDRGPU_OK;
+    }
+
+    int init(int dev, int sample_kind, int tap_kind, const void* taps, size_t ntaps,
+             uint32_t decim, size_t channels) {
+        if (!taps || ntaps == 0 || decim == 0 || channels == 0) return SDRGPU_ERR_INVALID;
+        if (ntaps > (1u << 20) || decim > (1u << 20) || channels > (1u << 24))
+            return SDRGPU_ERR_UNSUPPORTED;
+        if (!((sample_kind == SDRGPU_F32 && tap_kind == SDRGPU_F32) ||
+              (sample_kind == SDRGPU_C64 && tap_kind == SDRGPU_F32) ||
+              (sample_kind == SDRGPU_C64 && tap_kind == SDRGPU_C64)))
+            return SDRGPU_ERR_INVALID;
+        int st = check_device(dev);
+        if (st) return st;
+        device = dev;
+        sk = sample_kind;
+        tk = tap_kind;
+        K = (int)ntaps;
+        D = (int)decim;
+        nch = channels;
+        const size_t tb = kind_bytes(tk);
+        taps_host.assign((const unsigned char*)taps, (const unsigned char*)taps + tb * ntaps);
+
+        DeviceGuard g(device);
+        if (!g.ok()) return SDRGPU_ERR_DEVICE;
+        if ((st = stream.create())) return st;
+        // polyphase-major padded taps: taps_pm[p*tpp + i] = h[p + i*D]
+        tpp = taps_per_phase(K, D);
+        std::vector<unsigned char> pm((size_t)D * tpp * tb, 0);
+        for (int k = 0; k < K; ++k)
+            std::memcpy(&pm[((size_t)(k % D) * tpp + k / D) * tb], &taps_host[(size_t)k * tb], tb);
+        SDRGPU_HIP_TRY(hipMalloc(&d_taps_pm, pm.size()));
+        SDRGPU_HIP_TRY(hipMemcpy(d_taps_pm, pm.data(), pm.size(), hipMemcpyHostToDevice));
+        if (K > 1) {
+            SDRGPU_HIP_TRY(hipMalloc(&d_hist[0], hist_bytes()));
+            SDRGPU_HIP_TRY(hipMalloc(&d_hist[1], hist_bytes()));
+        }
+        return reset_state();
+    }
+
+    bool want_os() const {
+        if (algo == SDRGPU_FIR_DIRECT) return false;
+        if (!fir_os_supported(sk, tk, K, D)) return false;
+        return true;  // AUTO or OVERLAP_SAVE
+    }
+
+    // Enqueue one block (device pointers) on the current stream.
+    int run_dev(const void* d_in, size_t ld_in, size_t n_in, void* d_out, size_t ld_out,
+                size_t* n_out_ret) {
+        const size_t n_out = out_len(n_in);
+        if (n_out_ret) *n_out_ret = n_out;
+        if (n_in == 0) return SDRGPU_OK;
+        if (!d_in || (n_out > 0 && !d_out)) return SDRGPU_ERR_INVALID;
+        FirParams p{};
+        p.sample_kind = sk;
+        p.tap_kind = tk;
+        p.in = d_in;
+        p.ld_in = (long)ld_in;
+        p.n_in = (long)n_in;
+        // K == 1 has no history: point both at a harmless non-null buffer.
+        p.hist = K > 1 ? d_hist[cur] : d_taps_pm;
+        p.hist_next = K > 1 ? d_hist[cur ^ 1] : nullptr;
+        p.i0 = first_kept();
+        p.n_out = (long)n_out;
+        p.K = K;
+        p.D = D;
+        p.taps_pm = d_taps_pm;
+        p.tpp = tpp;
+        p.out = d_out;
+        p.ld_out = (long)ld_out;
+        p.nch = (int)nch;
+        p.force_naive = 0;
+        int st = SDRGPU_ERR_UNSUPPORTED;
+        if (want_os()) {
+            if (!os_state && os_status == SDRGPU_OK)
+                os_state = fir_os_prepare(device, sk, tk, taps_host.data(), K, D, stream.cur,
+                                          &os_status);
+            if (os_state) st = fir_os_launch(p, os_state, stream.cur);
+            if (st != SDRGPU_OK && algo == SDRGPU_FIR_OVERLAP_SAVE) return st;
+        }
+        if (st != SDRGPU_OK) st = fir_direct_launch(p, stream.cur);
+        if (st) return st;
+        if (K > 1) cur ^= 1;
+        seen += n_in;
+        return SDRGPU_OK;
+    }
+
+    int process_host(const void* in, size_t ld_in, size_t n_in, void* out, size_t ld_out,
+                     size_t out_cap, size_t* n_out_ret) {
+        const size_t n_out = out_len(n_in);
+        if (n_out_ret) *n_out_ret = n_out;
+        if (n_out > out_cap) return SDRGPU_ERR_OUTPUT_CAP;
+        if (n_in == 0) return SDRGPU_OK;
+        if (!in || (n_out && !out)) return SDRGPU_ERR_INVALID;
+        DeviceGuard g(device);
+        if (!g.ok()) return SDRGPU_ERR_DEVICE;
+        const size_t sb = sbytes();
+        int st;
+        // Stage densely (leading dimension = n_in / n_out on the device).
+        if ((st = stage_in.ensure(nch * n_in * sb))) return st;
+        if ((st = stage_out.ensure(nch * (n_out ? n_out : 1) * sb))) return st;
+        SDRGPU_HIP_TRY(hipMemcpy2DAsync(stage_in.ptr, n_in * sb, in, ld_in * sb, n_in * sb, nch,
+                                        hipMemcpyHostToDevice, stream.cur));
+        size_t got = 0;
+        if ((st = run_dev(stage_in.ptr, n_in, n_in, stage_out.ptr, n_out, &got))) return st;
+        if (n_out)
+            SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * sb, stage_out.ptr, n_out * sb,
+                                            n_out * sb, nch, hipMemcpyDeviceToHost, stream.cur));
+        SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
+        return SDRGPU_OK;
+    }
+
+    int clone_into(FirCore* dst) const {
+        int st = dst->init(device, sk, tk, taps_host.data(), (size_t)K, (uint32_t)D, nch);
+        if (st) return st;
+        DeviceGuard g(device);
+        dst->algo = algo;
+        dst->seen = seen;
+        dst->cur = 0;
+        if (K > 1) {
+            SDRGPU_HIP_TRY(hipMemcpyAsync(dst->d_hist[0], d_hist[cur], hist_bytes(),
+                                          hipMemcpyDeviceToDevice, stream.cur));
+            SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
+        }
+        return SDRGPU_OK;
+    }
+};
+
+struct sdrgpu_fir {
+    FirCore core;
+};
+struct sdrgpu_firbank {
+    FirCore core;
+};
+
+extern "C" {
+
+// ------------------------------- single stream -------------------------------------
+int sdrgpu_fir_create(int device, int sample_kind, int tap_kind, const void* taps,
+                      size_t ntaps, uint32_t decim, sdrgpu_fir** out) {
+    if (!out) return SDRGPU_ERR_INVALID;
+    *out = nullptr;
+    auto* h = new (std::nothrow) sdrgpu_fir();
+    if (!h) return SDRGPU_ERR_NOMEM;
+    int st = h->core.init(device, sample_kind, tap_kind, taps, ntaps, decim, 1);
+    if (st) {
+        h->core.free_all();
+        delete h;
+        return st;
+    }
+    *out = h;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_fir_set_algorithm(sdrgpu_fir* h, int algo) {
+    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_OVERLAP_SAVE) return SDRGPU_ERR_INVALID;
+    if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
+        !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        return SDRGPU_ERR_UNSUPPORTED;
+    h->core.algo = algo;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_fir_set_stream(sdrgpu_fir* h, void* s) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    h->core.stream.set(s);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_fir_output_len(const sdrgpu_fir* h, size_t n_in, size_t* n_out) {
+    if (!h || !n_out) return SDRGPU_ERR_INVALID;
+    *n_out = h->core.out_len(n_in);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out, size_t out_cap,
+                       size_t* n_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    return h->core.process_host(in, n_in, n_in, out, out_cap, out_cap, n_out);
+}
+
+int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d_out,
+                           size_t out_cap, size_t* n_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    const size_t need = h->core.out_len(n_in);
+    if (n_out) *n_out = need;
+    if (need > out_cap) return SDRGPU_ERR_OUTPUT_CAP;
+    DeviceGuard g(h->core.device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    return h->core.run_dev(d_in, n_in, n_in, d_out, out_cap, n_out);
+}
+
+int sdrgpu_fir_sync(sdrgpu_fir* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->core.device);
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->core.stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_fir_reset(sdrgpu_fir* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    return h->core.reset_state();
+}
+
+int sdrgpu_fir_clone(const sdrgpu_fir* h, sdrgpu_fir** out) {
+    if (!h || !out) return SDRGPU_ERR_INVALID;
+    *out = nullptr;
+    auto* c = new (std::nothrow) sdrgpu_fir();
+    if (!c) return SDRGPU_ERR_NOMEM;
+    int st = h->core.clone_into(&c->core);
+    if (st) {
+        c->core.free_all();
+        delete c;
+        return st;
+    }
+    *out = c;
+    return SDRGPU_OK;
+}
+
+void sdrgpu_fir_destroy(sdrgpu_fir* h) {
+    if (!h) return;
+    h->core.free_all();
+    delete h;
+}
+
+// ------------------------------- FIR bank ------------------------------------------
+int sdrgpu_firbank_create(int device, int sample_kind, int tap_kind, const void* taps,
+                          size_t ntaps, uint32_t decim, size_t nch, sdrgpu_firbank** out) {
+    if (!out) return SDRGPU_ERR_INVALID;
+    *out = nullptr;
+    auto* h = new (std::nothrow) sdrgpu_firbank();
+    if (!h) return SDRGPU_ERR_NOMEM;
+    int st = h->core.init(device, sample_kind, tap_kind, taps, ntaps, decim, nch);
+    if (st) {
+        h->core.free_all();
+        delete h;
+        return st;
+    }
+    *out = h;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo) {
+    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_OVERLAP_SAVE) return SDRGPU_ERR_INVALID;
+    if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
+        !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        return SDRGPU_ERR_UNSUPPORTED;
+    h->core.algo = algo;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_set_stream(sdrgpu_firbank* h, void* s) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    h->core.stream.set(s);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_output_len(const sdrgpu_firbank* h, size_t n_in, size_t* n_out) {
+    if (!h || !n_out) return SDRGPU_ERR_INVALID;
+    *n_out = h->core.out_len(n_in);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_process(sdrgpu_firbank* h, const void* in, size_t ld_in, size_t n_in,
+                           void* out, size_t ld_out, size_t* n_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    const size_t need = h->core.out_len(n_in);
+    if (ld_in < n_in || (need && ld_out < need)) return SDRGPU_ERR_INVALID;
+    return h->core.process_host(in, ld_in, n_in, out, ld_out, ld_out, n_out);
+}
+
+int sdrgpu_firbank_process_dev(sdrgpu_firbank* h, const void* d_in, size_t ld_in, size_t n_in,
+                               void* d_out, size_t ld_out, size_t* n_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    const size_t need = h->core.out_len(n_in);
+    if (n_out) *n_out = need;
+    if (ld_in < n_in || (need && ld_out < need)) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->core.device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    return h->core.run_dev(d_in, ld_in, n_in, d_out, ld_out, n_out);
+}
+
+int sdrgpu_firbank_sync(sdrgpu_firbank* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->core.device);
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->core.stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_reset(sdrgpu_firbank* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    return h->core.reset_state();
+}
+
+int sdrgpu_firbank_clone(const sdrgpu_firbank* h, sdrgpu_firbank** out) {
+    if (!h || !out) return SDRGPU_ERR_INVALID;
+    *out = nullptr;
+    auto* c = new (std::nothrow) sdrgpu_firbank();
+    if (!c) return SDRGPU_ERR_NOMEM;
+    int st = h->core.clone_into(&c->core);
+    if (st) {
+        c->core.free_all();
+        delete c;
+        return st;
+    }
+    *out = c;
+    return SDRGPU_OK;
+}
+
+void sdrgpu_firbank_destroy(sdrgpu_firbank* h) {
+    if (!h) return;
+    h->core.free_all();
+    delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,42 @@
+// fir_kernels.hpp -- internal launch interface of the FIR kernels (not part of the ABI).
+#pragma once
+
+#include "common.hpp"
+
+namespace sdrgpu {
+
+// Taps are kept on the device in polyphase-major order: taps_pm[p*tpp + i] = h[p + i*D]
+// (zero beyond K), tpp = ceil(ceil(K/D) / 8) * 8.
+constexpr int kTapPad = 8;
+
+inline int taps_per_phase(int K, int D) {
+    int t = (K + D - 1) / D;
+    return (t + kTapPad - 1) / kTapPad * kTapPad;
+}
+
+struct FirParams {
+    int sample_kind, tap_kind;
+    const void* in;       // device, channel c at in + c*ld_in samples
+    long ld_in;
+    long n_in;            // samples this call, per channel
+    const void* hist;     // device, nch x (K-1): stream samples -(K-1)..-1
+    void* hist_next;      // device, written with the new history
+    long i0;              // local index of the first kept output
+    long n_out;           // kept outputs this call, per channel
+    int K, D;
+    const void* taps_pm;  // device, polyphase-major padded taps
+    int tpp;
+    void* out;            // device, channel c at out + c*ld_out samples
+    long ld_out;
+    int nch;
+    int force_naive;
+};
+
+int fir_direct_launch(const FirParams& p, hipStream_t s);
+
+// Overlap-save (polyphase, LDS-resident FFT) path; returns SDRGPU_ERR_UNSUPPORTED for
+// shapes it does not cover (caller falls back to direct).
+struct FirOsPlan;
+int fir_os_supported(int sample_kind, int tap_kind, int K, int D);
+
+}  // namespace sdrgpu

@@ -1,0 +1,14 @@
+"""sdrgpu -- MI355X-native FIR / FFT / PLL sample-stream core (host-side mirror).
+
+Mirrors the reference crate's `filter`, `fft` and `signal` API (agrif/unnamed-rust-sdr,
+src/filter/mod.rs, src/fft.rs, src/signal/mod.rs) over the C ABI in include/sdrgpu.h.
+All compute runs in libsdrgpu.so (hand-written HIP for gfx950); importing this package
+without the built library raises ImportError.
+"""
+from . import _lib
+from ._lib import C64, F32, SdrGpuError, device_count, lib
+from . import filter  # noqa: F401
+
+lib()  # fail loudly at import if the HIP library is missing
+
+__all__ = ["filter", "C64", "F32", "SdrGpuError", "device_count", "lib"]

@@ -1,0 +1,379 @@
+"""Host-side mirror of the reference `filter` module over the sdrgpu C ABI.
+
+Reference interface (agrif/unnamed-rust-sdr):
+  trait Filter<A>        { fn apply(&mut self, A) -> Output }      src/filter/mod.rs:23-26
+  trait FilterDesign<A>  { fn design(self, rate) -> Filter;
+                           fn design_for(self, &signal) }          src/filter/mod.rs:28-39
+  Fir / Vec<C> / &[C] designs                                       src/filter/fir.rs:36-58
+  BiquadD::{LowPass,HighPass,BandPass,Notch,Lr}                     src/filter/biquad.rs:63-155
+  Identity                                                          src/filter/simple.rs:3-19
+  PllDesign::new(reference, gain, loop, output, lock)               src/filter/pll.rs:25-37
+
+Names and argument meaning follow the reference.  Designs are plain values; `design(rate)`
+returns a GPU-backed filter handle.  Because a per-sample FFI call is infeasible, handles
+process BLOCKS (`process`) -- `apply` exists for API parity and is a one-sample block.
+State carries across blocks, so any block partition yields the reference's sample-by-
+sample result.  Handles are Send-not-Sync like the reference filters.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import C64, F32, check, lib
+
+
+def _kind_of(arr: np.ndarray) -> int:
+    if np.iscomplexobj(arr):
+        return C64
+    return F32
+
+
+def _as_c(arr, kind: int) -> np.ndarray:
+    if kind == C64:
+        return np.ascontiguousarray(arr, dtype=np.complex64)
+    return np.ascontiguousarray(arr, dtype=np.float32)
+
+
+def _np_dtype(kind: int):
+    return np.complex64 if kind == C64 else np.float32
+
+
+# ------------------------------------------------------------------------------ FIR
+class Fir:
+    """FilterDesign for FIR taps: `Fir::new(coef)` / `Vec<C>` / `&[C]` (fir.rs:12-58).
+
+    `decim` (default 1) fuses the reference's `.decimate(rate)` adapter that usually
+    follows (signal/adapters/mod.rs:13-41): only outputs at stream indices D-1, 2D-1, ...
+    are produced.  `sample_kind` selects f32 or Complex<f32> samples (the reference infers
+    A from the signal; design_for() does the same here)."""
+
+    def __init__(self, coef: Union[Sequence, np.ndarray], decim: int = 1,
+                 sample_kind: Optional[int] = None, device: int = 0,
+                 algorithm: int = _lib.FIR_AUTO):
+        coef = np.asarray(coef)
+        if coef.ndim != 1 or coef.size == 0:
+            raise _lib.SdrGpuError(_lib.ERR_INVALID, "Fir: taps must be a non-empty 1-D array")
+        self.tap_kind = _kind_of(coef)
+        self.coef = _as_c(coef, self.tap_kind)
+        self.decim = int(decim)
+        self.sample_kind = sample_kind
+        self.device = device
+        self.algorithm = algorithm
+
+    def with_decim(self, decim: int) -> "Fir":
+        return Fir(self.coef, decim, self.sample_kind, self.device, self.algorithm)
+
+    def design(self, rate: float = 0.0, sample_kind: Optional[int] = None) -> "FirFilter":
+        """FilterDesign::design -- rate is unused for FIR (fir.rs:39)."""
+        sk = sample_kind if sample_kind is not None else self.sample_kind
+        if sk is None:
+            sk = C64 if self.tap_kind == C64 else F32
+        return FirFilter(self.coef, sk, self.decim, self.device, self.algorithm)
+
+    def design_for(self, signal) -> "FirFilter":
+        return self.design(signal.rate(), getattr(signal, "sample_kind", None))
+
+
+class FirFilter:
+    """GPU Fir<C, A> handle (fir.rs:6-32) with optional fused decimation."""
+
+    def __init__(self, coef: np.ndarray, sample_kind: int, decim: int = 1, device: int = 0,
+                 algorithm: int = _lib.FIR_AUTO, _handle=None):
+        self.sample_kind = sample_kind
+        self.tap_kind = _kind_of(coef)
+        self.coef = coef
+        self.decim = decim
+        self.device = device
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib().sdrgpu_fir_create(device, sample_kind, self.tap_kind,
+                                          coef.ctypes.data, coef.size, decim,
+                                          ctypes.byref(self._h)), "sdrgpu_fir_create")
+        if algorithm != _lib.FIR_AUTO:
+            self.set_algorithm(algorithm)
+
+    # -- handle management (SampleRate-style, resample.rs:32-110) --
+    def close(self):
+        if self._h:
+            lib().sdrgpu_fir_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def clone(self) -> "FirFilter":
+        h = ctypes.c_void_p()
+        check(lib().sdrgpu_fir_clone(self._h, ctypes.byref(h)), "sdrgpu_fir_clone")
+        return FirFilter(self.coef, self.sample_kind, self.decim, self.device, _handle=h)
+
+    def reset(self):
+        check(lib().sdrgpu_fir_reset(self._h), "sdrgpu_fir_reset")
+
+    def set_algorithm(self, algo: int):
+        check(lib().sdrgpu_fir_set_algorithm(self._h, algo), "sdrgpu_fir_set_algorithm")
+
+    def set_stream(self, stream_ptr: Optional[int]):
+        check(lib().sdrgpu_fir_set_stream(self._h, stream_ptr), "sdrgpu_fir_set_stream")
+
+    def output_len(self, n_in: int) -> int:
+        n = ctypes.c_size_t()
+        check(lib().sdrgpu_fir_output_len(self._h, n_in, ctypes.byref(n)), "output_len")
+        return n.value
+
+    # -- processing --
+    def process(self, x) -> np.ndarray:
+        """Filter one block of host samples; returns the (kept) outputs."""
+        x = _as_c(x, self.sample_kind)
+        n_out = self.output_len(x.size)
+        out = np.empty(max(n_out, 1), dtype=_np_dtype(self.sample_kind))
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_fir_process(self._h, x.ctypes.data, x.size, out.ctypes.data,
+                                       out.size, ctypes.byref(got)), "sdrgpu_fir_process")
+        return out[:got.value]
+
+    def apply(self, value):
+        """Filter::apply for one sample (fir.rs:23-32).  Returns None when decimation
+        drops the sample (the Decimate adapter would skip it)."""
+        y = self.process(np.asarray([value]))
+        return y[0] if y.size else None
+
+    def process_dev(self, d_in_ptr: int, n_in: int, d_out_ptr: int, out_cap: int) -> int:
+        """Enqueue on the handle's stream with device pointers; returns n_out."""
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_fir_process_dev(self._h, d_in_ptr, n_in, d_out_ptr, out_cap,
+                                           ctypes.byref(got)), "sdrgpu_fir_process_dev")
+        return got.value
+
+    def sync(self):
+        check(lib().sdrgpu_fir_sync(self._h), "sdrgpu_fir_sync")
+
+
+class FirBank:
+    """nch independent Fir<C,A> (fir.rs:6-32) sharing taps; channel-major blocks."""
+
+    def __init__(self, coef, nch: int, sample_kind: int = C64, decim: int = 1,
+                 device: int = 0, algorithm: int = _lib.FIR_AUTO, _handle=None):
+        coef = np.asarray(coef)
+        self.tap_kind = _kind_of(coef)
+        self.coef = _as_c(coef, self.tap_kind)
+        self.nch = nch
+        self.sample_kind = sample_kind
+        self.decim = decim
+        self.device = device
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib().sdrgpu_firbank_create(device, sample_kind, self.tap_kind,
+                                              self.coef.ctypes.data, self.coef.size, decim,
+                                              nch, ctypes.byref(self._h)),
+                  "sdrgpu_firbank_create")
+        if algorithm != _lib.FIR_AUTO:
+            self.set_algorithm(algorithm)
+
+    def close(self):
+        if self._h:
+            lib().sdrgpu_firbank_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def clone(self) -> "FirBank":
+        h = ctypes.c_void_p()
+        check(lib().sdrgpu_firbank_clone(self._h, ctypes.byref(h)), "sdrgpu_firbank_clone")
+        return FirBank(self.coef, self.nch, self.sample_kind, self.decim, self.device,
+                       _handle=h)
+
+    def reset(self):
+        check(lib().sdrgpu_firbank_reset(self._h), "sdrgpu_firbank_reset")
+
+    def set_algorithm(self, algo: int):
+        check(lib().sdrgpu_firbank_set_algorithm(self._h, algo), "set_algorithm")
+
+    def set_stream(self, stream_ptr: Optional[int]):
+        check(lib().sdrgpu_firbank_set_stream(self._h, stream_ptr), "set_stream")
+
+    def output_len(self, n_in: int) -> int:
+        n = ctypes.c_size_t()
+        check(lib().sdrgpu_firbank_output_len(self._h, n_in, ctypes.byref(n)), "output_len")
+        return n.value
+
+    def process(self, x) -> np.ndarray:
+        """x: (nch, n) host array -> (nch, n_out)."""
+        x = _as_c(x, self.sample_kind)
+        if x.ndim != 2 or x.shape[0] != self.nch:
+            raise _lib.SdrGpuError(_lib.ERR_INVALID, "FirBank.process: shape must be (nch, n)")
+        n_in = x.shape[1]
+        n_out = self.output_len(n_in)
+        out = np.empty((self.nch, max(n_out, 1)), dtype=_np_dtype(self.sample_kind))
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_firbank_process(self._h, x.ctypes.data, n_in, n_in,
+                                           out.ctypes.data, out.shape[1], ctypes.byref(got)),
+              "sdrgpu_firbank_process")
+        return out[:, :got.value]
+
+    def process_dev(self, d_in_ptr: int, ld_in: int, n_in: int, d_out_ptr: int,
+                    ld_out: int) -> int:
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_firbank_process_dev(self._h, d_in_ptr, ld_in, n_in, d_out_ptr,
+                                               ld_out, ctypes.byref(got)),
+              "sdrgpu_firbank_process_dev")
+        return got.value
+
+    def sync(self):
+        check(lib().sdrgpu_firbank_sync(self._h), "sdrgpu_firbank_sync")
+
+
+# --------------------------------------------------------------------------- Biquad
+@dataclass(frozen=True)
+class BiquadD:
+    """BiquadD enum (biquad.rs:63-71).  Construct with the class helpers below."""
+    kind: int
+    freq: float
+    q: float = 0.0
+
+    @staticmethod
+    def LowPass(freq: float, q: float) -> "BiquadD":
+        return BiquadD(_lib.BQ_LOWPASS, freq, q)
+
+    @staticmethod
+    def HighPass(freq: float, q: float) -> "BiquadD":
+        return BiquadD(_lib.BQ_HIGHPASS, freq, q)
+
+    @staticmethod
+    def BandPass(freq: float, q: float) -> "BiquadD":
+        return BiquadD(_lib.BQ_BANDPASS, freq, q)
+
+    @staticmethod
+    def Notch(freq: float, q: float) -> "BiquadD":
+        return BiquadD(_lib.BQ_NOTCH, freq, q)
+
+    @staticmethod
+    def Lr(decayrate: float) -> "BiquadD":
+        return BiquadD(_lib.BQ_LR, decayrate, 0.0)
+
+    def to_c(self) -> _lib.BiquadDesignC:
+        return _lib.BiquadDesignC(self.kind, self.freq, self.q)
+
+
+class _IdentityType:
+    """filter::Identity (simple.rs:3-19)."""
+    kind = _lib.BQ_IDENTITY
+    freq = 0.0
+    q = 0.0
+
+    def to_c(self) -> _lib.BiquadDesignC:
+        return _lib.BiquadDesignC(_lib.BQ_IDENTITY, 0.0, 0.0)
+
+    def __repr__(self):
+        return "Identity"
+
+
+Identity = _IdentityType()
+
+
+# ------------------------------------------------------------------------------ PLL
+class PllDesign:
+    """PllDesign::new(reference, gain, loopfilter, outputfilter, lockfilter)
+    (pll.rs:25-37).  design(rate) -> Pll over `nch` independent channels."""
+
+    def __init__(self, reference: float, gain: float, loopfilter, outputfilter, lockfilter):
+        self.reference = reference
+        self.gain = gain
+        self.loopfilter = loopfilter
+        self.outputfilter = outputfilter
+        self.lockfilter = lockfilter
+
+    def params(self, rate: float) -> _lib.PllParamsC:
+        return _lib.PllParamsC(self.reference, self.gain, rate, self.loopfilter.to_c(),
+                               self.outputfilter.to_c(), self.lockfilter.to_c())
+
+    def design(self, rate: float, nch: int = 1, device: int = 0) -> "Pll":
+        return Pll(self.params(rate), nch, device)
+
+
+class Pll:
+    """GPU Pll (pll.rs:12-22, 70-85), one per channel.  process() returns
+    (output, locked): output = Some(v) -> v, None -> 0.0 (main.rs:49)."""
+
+    def __init__(self, params: _lib.PllParamsC, nch: int = 1, device: int = 0, _handle=None):
+        self.params = params
+        self.nch = nch
+        self.device = device
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib().sdrgpu_pll_create(device, ctypes.byref(params), nch,
+                                          ctypes.byref(self._h)), "sdrgpu_pll_create")
+
+    def close(self):
+        if self._h:
+            lib().sdrgpu_pll_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def clone(self) -> "Pll":
+        h = ctypes.c_void_p()
+        check(lib().sdrgpu_pll_clone(self._h, ctypes.byref(h)), "sdrgpu_pll_clone")
+        return Pll(self.params, self.nch, self.device, _handle=h)
+
+    def reset(self):
+        check(lib().sdrgpu_pll_reset(self._h), "sdrgpu_pll_reset")
+
+    def set_stream(self, stream_ptr):
+        check(lib().sdrgpu_pll_set_stream(self._h, stream_ptr), "sdrgpu_pll_set_stream")
+
+    def process(self, x):
+        """x: (nch, n) or (n,) complex -> (out float32, locked uint8) of the same shape."""
+        x = np.ascontiguousarray(x, dtype=np.complex64)
+        squeeze = x.ndim == 1
+        if squeeze:
+            x = x[None, :]
+        if x.shape[0] != self.nch:
+            raise _lib.SdrGpuError(_lib.ERR_INVALID, "Pll.process: expected nch rows")
+        n = x.shape[1]
+        out = np.empty((self.nch, max(n, 1)), dtype=np.float32)
+        locked = np.empty((self.nch, max(n, 1)), dtype=np.uint8)
+        check(lib().sdrgpu_pll_process(self._h, x.ctypes.data, n, n, out.ctypes.data,
+                                       locked.ctypes.data, out.shape[1]), "sdrgpu_pll_process")
+        out, locked = out[:, :n], locked[:, :n]
+        return (out[0], locked[0]) if squeeze else (out, locked)
+
+    def apply(self, value):
+        """Filter::apply (pll.rs:70-85): Some(output) or None."""
+        o, l = self.process(np.asarray([value], dtype=np.complex64))
+        return float(o[0]) if l[0] else None
+
+    def process_dev(self, d_in, ld_in, n, d_out, d_locked, ld_out):
+        check(lib().sdrgpu_pll_process_dev(self._h, d_in, ld_in, n, d_out, d_locked, ld_out),
+              "sdrgpu_pll_process_dev")
+
+    def state(self, ch: int = 0):
+        """Public fields Pll::nphase, Pll::value (pll.rs:20-21)."""
+        nph = ctypes.c_float()
+        val = (ctypes.c_float * 2)()
+        check(lib().sdrgpu_pll_state(self._h, ch, ctypes.byref(nph), val), "sdrgpu_pll_state")
+        return nph.value, complex(val[0], val[1])
+
+    def sync(self):
+        check(lib().sdrgpu_pll_sync(self._h), "sdrgpu_pll_sync")
