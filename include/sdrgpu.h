@@ -65,6 +65,23 @@ const char* sdrgpu_strerror(int code);   /* resample::Error Display, src/resampl
 int sdrgpu_abi_version(void);
 int sdrgpu_device_count(int* count);
 
+/* ---- device memory, streams and timing ----
+ * The _dev entry points need device buffers; these helpers let a host without its own
+ * GPU runtime (the Rust crate, C callers, the Python mirror) allocate them.  No reference
+ * counterpart: the reference is CPU-only.  kind: 0 H2D, 1 D2H, 2 D2D. */
+enum sdrgpu_copy_kind { SDRGPU_H2D = 0, SDRGPU_D2H = 1, SDRGPU_D2D = 2 };
+int sdrgpu_dev_alloc(int device, size_t bytes, void** dptr);
+int sdrgpu_dev_free(int device, void* dptr);
+int sdrgpu_dev_copy(int device, void* dst, const void* src, size_t bytes, int kind);
+int sdrgpu_dev_memset(int device, void* dptr, int value, size_t bytes);
+int sdrgpu_dev_synchronize(int device);
+/* HIP events for timing work enqueued on a handle's stream (see *_get_stream). */
+int sdrgpu_event_create(int device, void** event);
+int sdrgpu_event_record(void* event, void* hip_stream);
+int sdrgpu_event_synchronize(void* event);
+int sdrgpu_event_elapsed_ms(void* start, void* end, float* ms);
+int sdrgpu_event_destroy(void* event);
+
 /* =====================================================================================
  * FIR / FIR-decimate.
  * Replaces: Fir::new / Fir::apply            (src/filter/fir.rs:12-32)
@@ -89,6 +106,7 @@ int sdrgpu_fir_create(int device, int sample_kind, int tap_kind, const void* tap
 int sdrgpu_fir_set_algorithm(sdrgpu_fir* h, int algo);
 /* Use an external hipStream_t (NULL restores the handle's own stream). */
 int sdrgpu_fir_set_stream(sdrgpu_fir* h, void* hip_stream);
+int sdrgpu_fir_get_stream(const sdrgpu_fir* h, void** hip_stream);
 /* Number of outputs the next process() call produces for n_in inputs. */
 int sdrgpu_fir_output_len(const sdrgpu_fir* h, size_t n_in, size_t* n_out);
 int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
@@ -109,6 +127,7 @@ int sdrgpu_firbank_create(int device, int sample_kind, int tap_kind, const void*
                           size_t ntaps, uint32_t decim, size_t nch, sdrgpu_firbank** out);
 int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo);
 int sdrgpu_firbank_set_stream(sdrgpu_firbank* h, void* hip_stream);
+int sdrgpu_firbank_get_stream(const sdrgpu_firbank* h, void** hip_stream);
 int sdrgpu_firbank_output_len(const sdrgpu_firbank* h, size_t n_in, size_t* n_out);
 int sdrgpu_firbank_process(sdrgpu_firbank* h, const void* in, size_t ld_in, size_t n_in,
                            void* out, size_t ld_out, size_t* n_out);
@@ -133,6 +152,7 @@ typedef struct sdrgpu_fft sdrgpu_fft;
 
 int sdrgpu_fft_plan(int device, size_t n, sdrgpu_fft** out);
 int sdrgpu_fft_set_stream(sdrgpu_fft* h, void* hip_stream);
+int sdrgpu_fft_get_stream(const sdrgpu_fft* h, void** hip_stream);
 int sdrgpu_fft_exec(sdrgpu_fft* h, const void* in, void* out, size_t count);
 int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t count);
 /* rfft: `count` frames of n F32 samples -> count frames of n/2 C64 bins [n/2, n). */
@@ -150,6 +170,7 @@ typedef struct sdrgpu_stft sdrgpu_stft;
 
 int sdrgpu_stft_create(int device, size_t n, size_t hop, sdrgpu_stft** out);
 int sdrgpu_stft_set_stream(sdrgpu_stft* h, void* hip_stream);
+int sdrgpu_stft_get_stream(const sdrgpu_stft* h, void** hip_stream);
 int sdrgpu_stft_output_len(const sdrgpu_stft* h, size_t n_in, size_t* n_frames);
 int sdrgpu_stft_process(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
                         size_t out_cap_frames, size_t* n_frames);
@@ -190,6 +211,7 @@ typedef struct sdrgpu_pll sdrgpu_pll;
 
 int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu_pll** out);
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
+int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** hip_stream);
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,
                        float* out, uint8_t* locked, size_t ld_out);
 int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t n,

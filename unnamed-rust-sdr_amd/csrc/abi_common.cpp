@@ -46,3 +46,103 @@ int sdrgpu_device_count(int* count) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------
+// Device memory / events (sdrgpu.h "device memory, streams and timing").
+extern "C" {
+
+int sdrgpu_dev_alloc(int device, size_t bytes, void** dptr) {
+    using namespace sdrgpu::detail;
+    if (!dptr) return SDRGPU_ERR_INVALID;
+    *dptr = nullptr;
+    int st = check_device(device);
+    if (st) return st;
+    DeviceGuard g(device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    SDRGPU_HIP_TRY(hipMalloc(dptr, bytes ? bytes : 1));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_dev_free(int device, void* dptr) {
+    using namespace sdrgpu::detail;
+    if (!dptr) return SDRGPU_OK;
+    DeviceGuard g(device);
+    SDRGPU_HIP_TRY(hipFree(dptr));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_dev_copy(int device, void* dst, const void* src, size_t bytes, int kind) {
+    using namespace sdrgpu::detail;
+    if ((!dst || !src) && bytes) return SDRGPU_ERR_INVALID;
+    hipMemcpyKind k;
+    switch (kind) {
+    case SDRGPU_H2D: k = hipMemcpyHostToDevice; break;
+    case SDRGPU_D2H: k = hipMemcpyDeviceToHost; break;
+    case SDRGPU_D2D: k = hipMemcpyDeviceToDevice; break;
+    default: return SDRGPU_ERR_INVALID;
+    }
+    if (!bytes) return SDRGPU_OK;
+    DeviceGuard g(device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    SDRGPU_HIP_TRY(hipMemcpy(dst, src, bytes, k));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_dev_memset(int device, void* dptr, int value, size_t bytes) {
+    using namespace sdrgpu::detail;
+    if (!dptr && bytes) return SDRGPU_ERR_INVALID;
+    if (!bytes) return SDRGPU_OK;
+    DeviceGuard g(device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    SDRGPU_HIP_TRY(hipMemset(dptr, value, bytes));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_dev_synchronize(int device) {
+    using namespace sdrgpu::detail;
+    int st = check_device(device);
+    if (st) return st;
+    DeviceGuard g(device);
+    SDRGPU_HIP_TRY(hipDeviceSynchronize());
+    return SDRGPU_OK;
+}
+
+int sdrgpu_event_create(int device, void** event) {
+    using namespace sdrgpu::detail;
+    if (!event) return SDRGPU_ERR_INVALID;
+    *event = nullptr;
+    int st = check_device(device);
+    if (st) return st;
+    DeviceGuard g(device);
+    hipEvent_t e;
+    SDRGPU_HIP_TRY(hipEventCreate(&e));
+    *event = e;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_event_record(void* event, void* stream) {
+    if (!event) return SDRGPU_ERR_INVALID;
+    SDRGPU_HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream)));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_event_synchronize(void* event) {
+    if (!event) return SDRGPU_ERR_INVALID;
+    SDRGPU_HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_event_elapsed_ms(void* start, void* end, float* ms) {
+    if (!start || !end || !ms) return SDRGPU_ERR_INVALID;
+    SDRGPU_HIP_TRY(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start),
+                                       static_cast<hipEvent_t>(end)));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_event_destroy(void* event) {
+    if (!event) return SDRGPU_OK;
+    SDRGPU_HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(event)));
+    return SDRGPU_OK;
+}
+
+}  // extern "C"

@@ -240,6 +240,12 @@ int sdrgpu_fir_set_stream(sdrgpu_fir* h, void* s) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_fir_get_stream(const sdrgpu_fir* h, void** s) {
+    if (!h || !s) return SDRGPU_ERR_INVALID;
+    *s = h->core.stream.cur;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_fir_output_len(const sdrgpu_fir* h, size_t n_in, size_t* n_out) {
     if (!h || !n_out) return SDRGPU_ERR_INVALID;
     *n_out = h->core.out_len(n_in);
@@ -325,6 +331,12 @@ int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo) {
 int sdrgpu_firbank_set_stream(sdrgpu_firbank* h, void* s) {
     if (!h) return SDRGPU_ERR_INVALID;
     h->core.stream.set(s);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_get_stream(const sdrgpu_firbank* h, void** s) {
+    if (!h || !s) return SDRGPU_ERR_INVALID;
+    *s = h->core.stream.cur;
     return SDRGPU_OK;
 }
 

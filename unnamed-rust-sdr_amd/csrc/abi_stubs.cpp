@@ -7,6 +7,9 @@ int sdrgpu_fft_set_stream(sdrgpu_fft*, void*) { return SDRGPU_ERR_UNSUPPORTED; }
 int sdrgpu_fft_exec(sdrgpu_fft*, const void*, void*, size_t) { return SDRGPU_ERR_UNSUPPORTED; }
 int sdrgpu_fft_exec_dev(sdrgpu_fft*, const void*, void*, size_t) { return SDRGPU_ERR_UNSUPPORTED; }
 int sdrgpu_rfft_exec(sdrgpu_fft*, const float*, void*, size_t) { return SDRGPU_ERR_UNSUPPORTED; }
+int sdrgpu_fft_get_stream(const sdrgpu_fft*, void**) { return SDRGPU_ERR_UNSUPPORTED; }
+int sdrgpu_stft_get_stream(const sdrgpu_stft*, void**) { return SDRGPU_ERR_UNSUPPORTED; }
+int sdrgpu_pll_get_stream(const sdrgpu_pll*, void**) { return SDRGPU_ERR_UNSUPPORTED; }
 int sdrgpu_fft_sync(sdrgpu_fft*) { return SDRGPU_ERR_UNSUPPORTED; }
 void sdrgpu_fft_destroy(sdrgpu_fft*) {}
 int sdrgpu_fft_freqs(size_t, float, float*) { return SDRGPU_ERR_UNSUPPORTED; }

@@ -68,10 +68,22 @@ SIGNATURES = [
     ("sdrgpu_strerror", c_char_p, [c_int]),
     ("sdrgpu_abi_version", c_int, []),
     ("sdrgpu_device_count", c_int, [POINTER(c_int)]),
+    # device memory / events
+    ("sdrgpu_dev_alloc", c_int, [c_int, c_size_t, _PH]),
+    ("sdrgpu_dev_free", c_int, [c_int, c_void_p]),
+    ("sdrgpu_dev_copy", c_int, [c_int, c_void_p, c_void_p, c_size_t, c_int]),
+    ("sdrgpu_dev_memset", c_int, [c_int, c_void_p, c_int, c_size_t]),
+    ("sdrgpu_dev_synchronize", c_int, [c_int]),
+    ("sdrgpu_event_create", c_int, [c_int, _PH]),
+    ("sdrgpu_event_record", c_int, [c_void_p, c_void_p]),
+    ("sdrgpu_event_synchronize", c_int, [c_void_p]),
+    ("sdrgpu_event_elapsed_ms", c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    ("sdrgpu_event_destroy", c_int, [c_void_p]),
     # FIR
     ("sdrgpu_fir_create", c_int, [c_int, c_int, c_int, c_void_p, c_size_t, c_uint32, _PH]),
     ("sdrgpu_fir_set_algorithm", c_int, [_H, c_int]),
     ("sdrgpu_fir_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_fir_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_fir_output_len", c_int, [_H, c_size_t, _PS]),
     ("sdrgpu_fir_process", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_process_dev", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
@@ -84,6 +96,7 @@ SIGNATURES = [
      [c_int, c_int, c_int, c_void_p, c_size_t, c_uint32, c_size_t, _PH]),
     ("sdrgpu_firbank_set_algorithm", c_int, [_H, c_int]),
     ("sdrgpu_firbank_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_firbank_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_firbank_output_len", c_int, [_H, c_size_t, _PS]),
     ("sdrgpu_firbank_process", c_int,
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, _PS]),
@@ -96,6 +109,7 @@ SIGNATURES = [
     # FFT
     ("sdrgpu_fft_plan", c_int, [c_int, c_size_t, _PH]),
     ("sdrgpu_fft_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_fft_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_fft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_fft_exec_dev", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_rfft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
@@ -105,6 +119,7 @@ SIGNATURES = [
     # STFT
     ("sdrgpu_stft_create", c_int, [c_int, c_size_t, c_size_t, _PH]),
     ("sdrgpu_stft_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_stft_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_stft_output_len", c_int, [_H, c_size_t, _PS]),
     ("sdrgpu_stft_process", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_stft_process_dev", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
@@ -114,6 +129,7 @@ SIGNATURES = [
     # PLL
     ("sdrgpu_pll_create", c_int, [c_int, POINTER(PllParamsC), c_size_t, _PH]),
     ("sdrgpu_pll_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_pll_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_pll_process", c_int,
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_pll_process_dev", c_int,

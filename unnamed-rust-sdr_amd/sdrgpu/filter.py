@@ -125,6 +125,11 @@ class FirFilter:
     def set_stream(self, stream_ptr: Optional[int]):
         check(lib().sdrgpu_fir_set_stream(self._h, stream_ptr), "sdrgpu_fir_set_stream")
 
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(lib().sdrgpu_fir_get_stream(self._h, ctypes.byref(s)), "sdrgpu_fir_get_stream")
+        return s.value or 0
+
     def output_len(self, n_in: int) -> int:
         n = ctypes.c_size_t()
         check(lib().sdrgpu_fir_output_len(self._h, n_in, ctypes.byref(n)), "output_len")
@@ -206,6 +211,11 @@ class FirBank:
 
     def set_stream(self, stream_ptr: Optional[int]):
         check(lib().sdrgpu_firbank_set_stream(self._h, stream_ptr), "set_stream")
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(lib().sdrgpu_firbank_get_stream(self._h, ctypes.byref(s)), "get_stream")
+        return s.value or 0
 
     def output_len(self, n_in: int) -> int:
         n = ctypes.c_size_t()
@@ -342,6 +352,11 @@ class Pll:
 
     def set_stream(self, stream_ptr):
         check(lib().sdrgpu_pll_set_stream(self._h, stream_ptr), "sdrgpu_pll_set_stream")
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(lib().sdrgpu_pll_get_stream(self._h, ctypes.byref(s)), "sdrgpu_pll_get_stream")
+        return s.value or 0
 
     def process(self, x):
         """x: (nch, n) or (n,) complex -> (out float32, locked uint8) of the same shape."""
