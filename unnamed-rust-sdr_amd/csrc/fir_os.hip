@@ -25,7 +25,9 @@
 //      kept outputs coalesced.  Stockham autosort order, twiddles from one 4096-entry
 //      table + recurrence.  LDS index padded (i + i/16, branch stride L + L/16 + 4) so
 //      every pass is (nearly) bank-conflict free.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -202,6 +204,215 @@ __global__ __launch_bounds__(kOsBlock) void fir_os_kernel(OsParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// v2 (D in {4, 8}, L = 4096/D <= 1024): persistent workgroups with software pipelining.
+// Each workgroup walks blocks q = blockIdx.x, +gridDim.x, ...; it issues the NEXT block's
+// 16 loads per lane as soon as the forward passes are done, so they fly under
+// I1..I5 of the current block (issued after P3, which is the last pass that loads
+// the branch spectra H from global: the hardware's in-order vmcnt would otherwise make
+// those loads wait for the prefetch).  Each pass's twiddle base is loaded once into
+// registers before the loop, so the inverse passes issue no VMEM load at all.  The inverse L-point FFT is radix-R3 from registers, then four radix-4
+// Stockham passes ping-ponging between two LDS regions with all 256 lanes busy.
+template <int D>
+__device__ __forceinline__ void os2_load(float2 (&v)[16], const float2* __restrict__ in,
+                                         const float2* __restrict__ hist, long n_in, int K,
+                                         long g0) {
+    if (g0 >= 0 && g0 + 256 * 15 < n_in) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = in[g0 + 256 * r];
+    } else {
+        // edge blocks (stream start with history, ragged tail): branch-free selects
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const long g = g0 + 256 * r;
+            const bool inb = (g >= 0) & (g < n_in);
+            const bool inh = (g < 0) & (g >= -(long)(K - 1));
+            const float2 x = in[inb ? g : 0];
+            const float2 xh = hist[inh ? g + (K - 1) : 0];
+            v[r] = inb ? x : (inh ? xh : make_float2(0.f, 0.f));
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long nblk) {
+    constexpr int L = kOsPoints / D;
+    constexpr int R3 = L / 256;
+    constexpr int LP = L + L / 16 + 4;
+    constexpr int NB = L / 16;   // forward radix-16 butterflies per branch
+    constexpr int NI = L / 4;    // inverse radix-4 butterflies (<= 256)
+    constexpr int IB = L + L / 16 + 8;  // offset of the second inverse buffer
+    static_assert(D * 16 * NB == 4096 && NI <= kOsBlock && 2 * IB <= D * LP, "geometry");
+    static_assert(NB % 16 == 0 && NI % 16 == 0, "padded strides need multiples of 16");
+    // padded offset of a multiple of 16: opad(i + n) = opad(i) + ps(n)
+    constexpr auto ps = [](int n) { return n + n / 16; };
+    __shared__ float2 lds[D * LP];
+    float2* const bufA = lds;
+    float2* const bufB = lds + IB;
+
+    const long ch = blockIdx.y;
+    const float2* __restrict__ in = p.in + ch * p.ld_in;
+    const float2* __restrict__ hist = p.hist + ch * (long)(p.K - 1);
+    float2* __restrict__ out = p.out + ch * p.ld_out;
+    const float2* __restrict__ tw = p.tw;
+    const int K = p.K;
+    const int skip = L - p.M;
+
+    // ---- per-lane twiddle bases (loaded once; the loop body loads only H and samples) ----
+    const int t0 = threadIdx.x;
+    const float2 w2b = tw[16 * ((t0 % NB) & 15)];
+    const float2 w3b = tw[t0 * D];
+    float2 wib[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int Ns = R3 << (2 * s);
+        const int k = (t0 % NI) % Ns;
+        wib[s] = conjf2(tw[k * (kOsPoints / (4 * Ns))]);
+    }
+
+    float2 v[16];
+    long q = blockIdx.x;
+    const long hop = (long)p.M * D;
+    long base = p.i0 + (q * p.M + p.M - L) * (long)D - (D - 1);
+    if (q < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + t0);
+
+#pragma unroll 1
+    for (; q < nblk; q += gridDim.x, base += hop * gridDim.x) {
+        // opaque per-iteration copy of the lane id: keeps the ~20 per-lane LDS/H address
+        // computations inside the loop instead of hoisting them into live registers
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        // same for the twiddle bases: their powers are recomputed per block (cheap VALU)
+        // rather than hoisted into ~60 loop-invariant registers
+        float2 w2 = w2b, w3 = w3b, wi[4] = {wib[0], wib[1], wib[2], wib[3]};
+        asm volatile("" : "+v"(w2.x), "+v"(w2.y), "+v"(w3.x), "+v"(w3.y));
+        asm volatile("" : "+v"(wi[0].x), "+v"(wi[0].y), "+v"(wi[1].x), "+v"(wi[1].y),
+                          "+v"(wi[2].x), "+v"(wi[2].y), "+v"(wi[3].x), "+v"(wi[3].y));
+
+        // ---- P1: radix-16 on the prefetched samples ----
+        Dft<16, false>::run(v);
+        {
+            const int b = D - 1 - (t % D), j = t / D;
+            float2* dst = lds + b * LP + 17 * j;           // opad(16 j + r) = 17 j + r
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[r] = v[r];
+        }
+        __syncthreads();
+
+        float2 u[16];
+        // ---- P2: radix-16, Ns = 16 ----
+        {
+            const int b = t / NB, j = t % NB;
+            float2* rd = lds + b * LP + opad(j);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) u[r] = rd[ps(NB) * r];
+            float2 wr = w2;
+#pragma unroll
+            for (int r = 1; r < 16; ++r) {
+                u[r] = cmul(u[r], wr);
+                if (r < 15) wr = cmul(wr, w2);
+            }
+            Dft<16, false>::run(u);
+            __syncthreads();
+            float2* wt = lds + b * LP + opad((j >> 4) * 256 + (j & 15));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) wt[17 * r] = u[r];
+        }
+        __syncthreads();
+
+        // ---- P3: radix-R3 per branch, multiply by H_b, sum over branches ----
+        float2 z[R3];
+#pragma unroll
+        for (int r = 0; r < R3; ++r) z[r] = make_float2(0.f, 0.f);
+        {
+            const float2* rd0 = lds + opad(t);
+            const float2* H = p.H + t;
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                float2 w[R3];
+#pragma unroll
+                for (int r = 0; r < R3; ++r) w[r] = rd0[b * LP + 272 * r];
+                float2 wr = w3;
+#pragma unroll
+                for (int r = 1; r < R3; ++r) {
+                    w[r] = cmul(w[r], wr);
+                    if (r + 1 < R3) wr = cmul(wr, w3);
+                }
+                Dft<R3, false>::run(w);
+#pragma unroll
+                for (int r = 0; r < R3; ++r) {
+                    const float2 h = H[b * L + 256 * r];
+                    z[r].x = fmaf(w[r].x, h.x, fmaf(-w[r].y, h.y, z[r].x));
+                    z[r].y = fmaf(w[r].x, h.y, fmaf(w[r].y, h.x, z[r].y));
+                }
+            }
+        }
+        // ---- prefetch the next block: flies under I1..I5 (no VMEM loads there) ----
+        if (q + gridDim.x < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + hop * gridDim.x + t);
+        __syncthreads();
+
+        // ---- I1: inverse radix-R3, Ns = 1 ----
+        Dft<R3, true>::run(z);
+        {
+            float2* wt = bufA + opad(t * R3);
+#pragma unroll
+            for (int r = 0; r < R3; ++r) wt[r] = z[r];
+        }
+        __syncthreads();
+
+        // ---- I2..I4: inverse radix-4, Ns = R3, 4R3, 16R3 (ping-pong A/B) ----
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int Ns = R3 << (2 * s);
+            const float2* src = (s & 1) ? bufB : bufA;
+            float2* dst = (s & 1) ? bufA : bufB;
+            if (t < NI) {
+                const int j = t, k = j % Ns;
+                const float2* rd = src + opad(j);
+                float2 a0 = rd[0], a1 = rd[ps(NI)], a2 = rd[2 * ps(NI)], a3 = rd[3 * ps(NI)];
+                const float2 w = wi[s], w2_ = cmul(w, w), w3_ = cmul(w2_, w);
+                a1 = cmul(a1, w);
+                a2 = cmul(a2, w2_);
+                a3 = cmul(a3, w3_);
+                dft4<true>(a0, a1, a2, a3);
+                const int o = (j / Ns) * 4 * Ns + k;
+                dst[opad(o)] = a0;
+                dst[opad(o + Ns)] = a1;
+                dst[opad(o + 2 * Ns)] = a2;
+                dst[opad(o + 3 * Ns)] = a3;
+            }
+            __syncthreads();
+        }
+
+        // ---- I5: inverse radix-4, Ns = L/4; outputs i = j + (L/4) r, stored coalesced ----
+        if (t < NI) {
+            const int j = t;
+            const float2* rd = bufB + opad(j);
+            float2 a0 = rd[0], a1 = rd[ps(NI)], a2 = rd[2 * ps(NI)], a3 = rd[3 * ps(NI)];
+            const float2 w = wi[3], w2_ = cmul(w, w), w3_ = cmul(w2_, w);
+            a1 = cmul(a1, w);
+            a2 = cmul(a2, w2_);
+            a3 = cmul(a3, w3_);
+            dft4<true>(a0, a1, a2, a3);
+            const long m0 = q * p.M - skip + j;
+            float2* o = out + m0;
+            if (j >= skip && m0 < p.n_out) o[0] = a0;
+            if (j + NI >= skip && m0 + NI < p.n_out) o[NI] = a1;
+            if (j + 2 * NI >= skip && m0 + 2 * NI < p.n_out) o[2 * NI] = a2;
+            if (j + 3 * NI >= skip && m0 + 3 * NI < p.n_out) o[3 * NI] = a3;
+        }
+        __syncthreads();  // I5 reads of bufB finish before the next P1 writes
+    }
+
+    if (blockIdx.x == gridDim.x - 1) {  // stream history carry (see fir_direct.hip)
+        float2* hn = p.hist_next + ch * (long)(K - 1);
+        for (int jj = t0; jj < K - 1; jj += kOsBlock) {
+            const long g = p.n_in - (long)(K - 1) + jj;
+            hn[jj] = g >= 0 ? in[g] : hist[g + (K - 1)];
+        }
+    }
+}
+
 struct OsState {
     int D = 1, L = 4096, M = 0, K = 1;
     float2* d_H = nullptr;
@@ -305,11 +516,22 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
     p.ld_out = fp.ld_out;
     const long nblk = fp.n_out > 0 ? ceil_div(fp.n_out, st->M) : 1;
     dim3 grid((unsigned)nblk, (unsigned)fp.nch);
+    // persistent grid for the pipelined v2 kernel: ~3 workgroups per CU in total
+    static const char* force_v1 = getenv("SDRGPU_OS_V1");
+    const long per_ch = std::max(1L, std::min(nblk, (256L * 3 + fp.nch - 1) / fp.nch));
+    dim3 pgrid((unsigned)per_ch, (unsigned)fp.nch);
+    const bool v2 = !(force_v1 && force_v1[0] == '1');
     switch (st->D) {
     case 1: hipLaunchKernelGGL(fir_os_kernel<1>, grid, dim3(kOsBlock), 0, s, p); break;
     case 2: hipLaunchKernelGGL(fir_os_kernel<2>, grid, dim3(kOsBlock), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(fir_os_kernel<4>, grid, dim3(kOsBlock), 0, s, p); break;
-    case 8: hipLaunchKernelGGL(fir_os_kernel<8>, grid, dim3(kOsBlock), 0, s, p); break;
+    case 4:
+        if (v2) hipLaunchKernelGGL(fir_os2_kernel<4>, pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else hipLaunchKernelGGL(fir_os_kernel<4>, grid, dim3(kOsBlock), 0, s, p);
+        break;
+    case 8:
+        if (v2) hipLaunchKernelGGL(fir_os2_kernel<8>, pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else hipLaunchKernelGGL(fir_os_kernel<8>, grid, dim3(kOsBlock), 0, s, p);
+        break;
     default: return SDRGPU_ERR_UNSUPPORTED;
     }
     SDRGPU_LAUNCH_CHECK();
