@@ -1,0 +1,217 @@
+// abi_pll.cpp -- C ABI of the batched PLL: PllDesign::new/design (reference
+// src/filter/pll.rs:25-60) with BiquadD designs (src/filter/biquad.rs:73-155) or Identity.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "abi_common.hpp"
+#include "pll_kernels.hpp"
+
+using namespace sdrgpu;
+using namespace sdrgpu::detail;
+
+namespace {
+
+// Biquad::new normalisation (biquad.rs:25-38)
+void bq_new(float a0, float a1, float a2, float b0, float b1, float b2, float* c) {
+    c[0] = b0 / a0;
+    c[1] = b1 / a0;
+    c[2] = b2 / a0;
+    c[3] = -a1 / a0;
+    c[4] = -a2 / a0;
+}
+
+// BiquadD::design (biquad.rs:83-155), host f32 math (glibc libm like Rust std).
+int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident) {
+    const float PI = 3.14159265358979323846f;
+    *ident = 0;
+    float omega, cs, alpha;
+    switch (d.kind) {
+    case SDRGPU_BQ_IDENTITY:
+        *ident = 1;
+        c[0] = 1.f; c[1] = c[2] = c[3] = c[4] = 0.f;
+        return SDRGPU_OK;
+    case SDRGPU_BQ_LOWPASS:
+        omega = 2.0f * PI * d.freq / rate; cs = cosf(omega); alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, (1.0f - cs) / 2.0f, 1.0f - cs, (1.0f - cs) / 2.0f, c);
+        return SDRGPU_OK;
+    case SDRGPU_BQ_HIGHPASS:
+        omega = 2.0f * PI * d.freq / rate; cs = cosf(omega); alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, (1.0f + cs) / 2.0f, -1.0f - cs, (1.0f + cs) / 2.0f, c);
+        return SDRGPU_OK;
+    case SDRGPU_BQ_BANDPASS:
+        omega = 2.0f * PI * d.freq / rate; cs = cosf(omega); alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, alpha, 0.0f, -alpha, c);
+        return SDRGPU_OK;
+    case SDRGPU_BQ_NOTCH:
+        omega = 2.0f * PI * d.freq / rate; cs = cosf(omega); alpha = sinf(omega) / (2.0f * d.q);
+        bq_new(1.0f + alpha, -2.0f * cs, 1.0f - alpha, 1.0f, -2.0f * cs, 1.0f, c);
+        return SDRGPU_OK;
+    case SDRGPU_BQ_LR: {
+        const float decayn = d.freq / rate;
+        bq_new(1.0f, -expf(-decayn), 0.0f, decayn, 0.0f, 0.0f, c);
+        return SDRGPU_OK;
+    }
+    default:
+        return SDRGPU_ERR_INVALID;
+    }
+}
+
+}  // namespace
+
+struct sdrgpu_pll {
+    int device = 0;
+    sdrgpu_pll_params params{};
+    PllDevParams dp{};
+    PllChannelState* d_state = nullptr;
+    StreamSlot stream;
+    DevBuf stage_in, stage_out, stage_lock;
+
+    void free_all() {
+        DeviceGuard g(device);
+        if (d_state) (void)hipFree(d_state);
+        d_state = nullptr;
+        stage_in.release();
+        stage_out.release();
+        stage_lock.release();
+        stream.destroy();
+    }
+};
+
+extern "C" {
+
+int sdrgpu_pll_reset(sdrgpu_pll* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    // PllDesign::design: nphase = 0, value = 0 + 0i, filter states zero (pll.rs:57-58)
+    SDRGPU_HIP_TRY(hipMemsetAsync(h->d_state, 0, h->dp.nch * sizeof(PllChannelState), h->stream.cur));
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu_pll** out) {
+    if (!out) return SDRGPU_ERR_INVALID;
+    *out = nullptr;
+    if (!p || nch == 0 || !(p->rate > 0.0f)) return SDRGPU_ERR_INVALID;
+    int st = check_device(device);
+    if (st) return st;
+    auto* h = new (std::nothrow) sdrgpu_pll();
+    if (!h) return SDRGPU_ERR_NOMEM;
+    h->device = device;
+    h->params = *p;
+    PllDevParams& d = h->dp;
+    d.nch = (long)nch;
+    d.rate = p->rate;
+    d.reference = p->reference / p->rate;  // pll.rs:51
+    d.gain = p->gain;
+    if ((st = bq_design(p->loopf, p->rate, d.loopc, &d.loop_ident)) ||
+        (st = bq_design(p->outputf, p->rate, d.outc, &d.out_ident)) ||
+        (st = bq_design(p->lockf, p->rate, d.lockc, &d.lock_ident))) {
+        delete h;
+        return st;
+    }
+    {
+        DeviceGuard g(device);
+        if (!g.ok()) st = SDRGPU_ERR_DEVICE;
+        if (!st) st = h->stream.create();
+        if (!st && hipMalloc(&h->d_state, nch * sizeof(PllChannelState)) != hipSuccess) st = SDRGPU_ERR_NOMEM;
+    }
+    if (!st) st = sdrgpu_pll_reset(h);
+    if (st) {
+        h->free_all();
+        delete h;
+        return st;
+    }
+    *out = h;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* s) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    h->stream.set(s);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** s) {
+    if (!h || !s) return SDRGPU_ERR_INVALID;
+    *s = h->stream.cur;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t n, float* d_out,
+                           uint8_t* d_locked, size_t ld_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    if (n == 0) return SDRGPU_OK;
+    if (!d_in || !d_out || !d_locked || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    return pll_launch(h->dp, static_cast<const float2*>(d_in), (long)ld_in, (long)n, d_out, d_locked,
+                      (long)ld_out, h->d_state, h->stream.cur);
+}
+
+int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, float* out,
+                       uint8_t* locked, size_t ld_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    if (n == 0) return SDRGPU_OK;
+    if (!in || !out || !locked || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    const size_t nch = (size_t)h->dp.nch;
+    int st;
+    if ((st = h->stage_in.ensure(nch * n * sizeof(float2))) ||
+        (st = h->stage_out.ensure(nch * n * sizeof(float))) ||
+        (st = h->stage_lock.ensure(nch * n)))
+        return st;
+    SDRGPU_HIP_TRY(hipMemcpy2DAsync(h->stage_in.ptr, n * sizeof(float2), in, ld_in * sizeof(float2),
+                                    n * sizeof(float2), nch, hipMemcpyHostToDevice, h->stream.cur));
+    if ((st = pll_launch(h->dp, static_cast<const float2*>(h->stage_in.ptr), (long)n, (long)n,
+                         static_cast<float*>(h->stage_out.ptr), static_cast<uint8_t*>(h->stage_lock.ptr),
+                         (long)n, h->d_state, h->stream.cur)))
+        return st;
+    SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(float), h->stage_out.ptr, n * sizeof(float),
+                                    n * sizeof(float), nch, hipMemcpyDeviceToHost, h->stream.cur));
+    SDRGPU_HIP_TRY(hipMemcpy2DAsync(locked, ld_out, h->stage_lock.ptr, n, n, nch, hipMemcpyDeviceToHost,
+                                    h->stream.cur));
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_state(sdrgpu_pll* h, size_t ch, float* nphase, float* value_re_im) {
+    if (!h || (long)ch >= h->dp.nch) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    PllChannelState s;
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    SDRGPU_HIP_TRY(hipMemcpy(&s, h->d_state + ch, sizeof(s), hipMemcpyDeviceToHost));
+    if (nphase) *nphase = s.nphase;
+    if (value_re_im) {
+        value_re_im[0] = s.vr;
+        value_re_im[1] = s.vi;
+    }
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_sync(sdrgpu_pll* h) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {
+    if (!h || !out) return SDRGPU_ERR_INVALID;
+    int st = sdrgpu_pll_create(h->device, &h->params, (size_t)h->dp.nch, out);
+    if (st) return st;
+    DeviceGuard g(h->device);
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    SDRGPU_HIP_TRY(hipMemcpy((*out)->d_state, h->d_state, h->dp.nch * sizeof(PllChannelState),
+                             hipMemcpyDeviceToDevice));
+    return SDRGPU_OK;
+}
+
+void sdrgpu_pll_destroy(sdrgpu_pll* h) {
+    if (!h) return;
+    h->free_all();
+    delete h;
+}
+
+}  // extern "C"

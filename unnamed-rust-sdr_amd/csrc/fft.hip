@@ -1,0 +1,401 @@
+// fft.hip -- batched Stockham FFT, four-step large FFT and STFT framing for gfx950.
+//
+// Semantics: fft::fft (reference src/fft.rs:3-28): forward DFT X[k] = sum x[n] e^{-2 pi i kn/N}
+// (rustfft FFTplanner::new(false)), then collated out[i] = X[(i - N/2) mod N] * (1/sqrt(N))
+// with the norm computed in f32 (fft.rs:16); rfft (fft.rs:30-37) keeps out[N/2..].  The STFT
+// framing is Window(N) + Decimate(hop) (src/signal/adapters/mod.rs:270-303, 13-41): frame j
+// covers stream samples [(j+1)hop - N, (j+1)hop), zero before the stream start.
+//
+// Kernels (256 lanes, 16 complex points per lane = one 4096-point LDS tile per workgroup):
+//   fft_tile_kernel  -- 4096/M transforms of size M <= 4096 per workgroup: coalesced load
+//                       (frame gather folded in), up to 3 radix-{2,4,8,16} Stockham passes in
+//                       LDS (twiddles from a 4096-entry table + recurrence), collated store.
+//   four-step (M > 4096, M = M1*M2): pass A = M2-point column FFTs on 4096/M2 columns per
+//                       workgroup (rows of 4096/M2 contiguous samples -> coalesced), times
+//                       W_M^{n1 k2}, to a scratch slab; pass B = M1-point FFTs over n1 on
+//                       4096/M1 consecutive k2, collated (shift + 1/sqrt(M)) store.  Frames are
+//                       processed in batches whose scratch slab stays in the 256 MiB MALL.
+// Roofline: HBM bound (C3: 24 algorithmic bytes per input sample, ~160 flop), see DESIGN.md.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "fft_device.hpp"
+#include "fft_kernels.hpp"
+
+namespace sdrgpu {
+
+using namespace fftd;
+
+namespace {
+
+constexpr int kFftBlock = 256;
+constexpr int kTile = 4096;
+__device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+constexpr int kTileLds = kTile + kTile / 16;
+
+// -------- frame sources ---------------------------------------------------------------
+struct FrameSrc {
+    // mode 0: contiguous frames (frame f at in + f*M)
+    // mode 1: STFT frames from a stream: frame f covers stream [f0 + (f+1)hop - M, +M), stream
+    //         index g < 0 -> hist[g + H] (H = history length) if g >= -H, else 0; g >= n_in -> 0
+    // mode 2: contiguous REAL frames (float, imag = 0) -- rfft
+    int mode;
+    const float2* in;
+    const float* in_real;
+    long n_in;
+    const float2* hist;
+    long H;
+    long first_end;  // stream index (exclusive end) of frame 0 of this launch
+    long hop;
+};
+
+__device__ __forceinline__ float2 frame_sample(const FrameSrc& s, long M, long f, long n) {
+    if (s.mode == 0) return s.in[f * M + n];
+    if (s.mode == 2) return make_float2(s.in_real[f * M + n], 0.f);
+    const long g = s.first_end + f * s.hop - M + n;
+    if (g >= 0) return g < s.n_in ? s.in[g] : make_float2(0.f, 0.f);
+    if (g >= -s.H) return s.hist[g + s.H];
+    return make_float2(0.f, 0.f);
+}
+
+// -------- generic in-place Stockham pass over the 4096-point tile ----------------------
+// batch of 4096/M transforms of size M; radix R; stride Ns.  Each lane does 16/R butterflies.
+template <int R, bool INV>
+__device__ __forceinline__ void tile_pass(float2* lds, int M, int Ns, const float2* __restrict__ tw) {
+    constexpr int NBF = 16 / R;
+    const int t = threadIdx.x;
+    const int bpt = M / R;  // butterflies per transform
+    float2 v[NBF][R];
+#pragma unroll
+    for (int u = 0; u < NBF; ++u) {
+        const int g = t * NBF + u;
+        const int f = g / bpt, j = g % bpt;
+        const int base = f * M;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[u][r] = lds[fpad(base + j + r * bpt)];
+        if (Ns > 1) {
+            const int k = j % Ns;
+            twiddle<R, INV>(v[u], tw, k * (kTile / (Ns * R)));
+        }
+        Dft<R, INV>::run(v[u]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NBF; ++u) {
+        const int g = t * NBF + u;
+        const int f = g / bpt, j = g % bpt;
+        const int k = j % Ns;
+        const int o = f * M + (j / Ns) * Ns * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[fpad(o + r * Ns)] = v[u][r];
+    }
+    __syncthreads();
+}
+
+template <bool INV>
+__device__ __forceinline__ void tile_fft(float2* lds, int M, const int* radix, int npass,
+                                         const float2* __restrict__ tw) {
+    int Ns = 1;
+    for (int p = 0; p < npass; ++p) {
+        switch (radix[p]) {
+        case 16: tile_pass<16, INV>(lds, M, Ns, tw); break;
+        case 8: tile_pass<8, INV>(lds, M, Ns, tw); break;
+        case 4: tile_pass<4, INV>(lds, M, Ns, tw); break;
+        default: tile_pass<2, INV>(lds, M, Ns, tw); break;
+        }
+        Ns *= radix[p];
+    }
+}
+
+struct TileArgs {
+    FrameSrc src;
+    long nframes;      // frames this launch
+    int M;
+    int radix[4];
+    int npass;
+    const float2* tw;  // W_4096
+    float norm;        // 1/sqrt(M) (f32, fft.rs:16)
+    int store_mode;    // 0: collated (fft), 1: upper half of collated (rfft)
+    float2* out;
+};
+
+__global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
+    __shared__ float2 lds[kTileLds];
+    const int t = threadIdx.x;
+    const int M = a.M;
+    const int fpt = kTile / M;  // frames per tile
+    const long f0 = (long)blockIdx.x * fpt;
+    const int nf = (int)min((long)fpt, a.nframes - f0);
+    // coalesced load: point p -> (frame p / M, sample p % M)
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + kFftBlock * i;
+        const int f = p / M, n = p % M;
+        float2 x = make_float2(0.f, 0.f);
+        if (f < nf) x = frame_sample(a.src, M, f0 + f, n);
+        lds[fpad(p)] = x;
+    }
+    __syncthreads();
+    tile_fft<false>(lds, M, a.radix, a.npass, a.tw);
+    // collated store: out[f][i] = X[(i + M/2) % M] * norm
+    const int half = M / 2;
+    if (a.store_mode == 0) {
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) {
+            const int p = t + kFftBlock * i;
+            const int f = p / M, o = p % M;
+            if (f < nf) {
+                int k = o + half;
+                if (k >= M) k -= M;
+                float2 x = lds[fpad(f * M + k)];
+                a.out[(f0 + f) * M + o] = make_float2(x.x * a.norm, x.y * a.norm);
+            }
+        }
+    } else {
+        // rfft: keep collated [M/2, M) = X[0, M/2)
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) {
+            const int p = t + kFftBlock * i;
+            const int f = p / M, k = p % M;
+            if (f < nf && k < half) {
+                float2 x = lds[fpad(f * M + k)];
+                a.out[(f0 + f) * half + k] = make_float2(x.x * a.norm, x.y * a.norm);
+            }
+        }
+    }
+}
+
+// -------- four-step, pass A: M2-point FFTs down the columns n1 of x[n1 + M1 n2] ---------
+struct FourArgs {
+    FrameSrc src;
+    long nframes;
+    int M, M1, M2;
+    int radixA[4], npassA;  // M2 = prod radixA
+    int radixB[4], npassB;  // M1 = prod radixB
+    const float2* tw;       // W_4096
+    const float2* twM;      // W_M, M entries
+    float norm;
+    float2* scratch;        // nframes x M: S[f][n1 * M2 + k2]
+    float2* out;
+};
+
+__global__ __launch_bounds__(kFftBlock) void fft4_pass_a(FourArgs a) {
+    __shared__ float2 lds[kTileLds];
+    const int t = threadIdx.x;
+    const int C = kTile / a.M2;                  // columns per workgroup
+    const int tiles_per_frame = a.M1 / C;
+    const long f = blockIdx.x / tiles_per_frame;
+    const int c0 = (int)(blockIdx.x % tiles_per_frame) * C;
+    if (f >= a.nframes) return;
+    // load: point p -> (n2 = p / C, col = p % C): row n2 holds C contiguous samples
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + kFftBlock * i;
+        const int n2 = p / C, col = p % C;
+        const float2 x = frame_sample(a.src, a.M, f, (long)(c0 + col) + (long)a.M1 * n2);
+        lds[fpad(col * a.M2 + n2)] = x;           // column-major: transform per column
+    }
+    __syncthreads();
+    tile_fft<false>(lds, a.M2, a.radixA, a.npassA, a.tw);
+    // twiddle W_M^{n1 k2}, store S[n1][k2] (consecutive k2 contiguous)
+    float2* S = a.scratch + f * (long)a.M;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + kFftBlock * i;
+        const int col = p / a.M2, k2 = p % a.M2;
+        const int n1 = c0 + col;
+        float2 x = lds[fpad(col * a.M2 + k2)];
+        const long e = ((long)n1 * k2) % a.M;
+        x = cmul(x, a.twM[e]);
+        S[(long)n1 * a.M2 + k2] = x;
+    }
+}
+
+// -------- four-step, pass B: M1-point FFTs over n1 for 4096/M1 consecutive k2 ----------
+__global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
+    __shared__ float2 lds[kTileLds];
+    const int t = threadIdx.x;
+    const int C = kTile / a.M1;                  // k2 columns per workgroup
+    const int tiles_per_frame = a.M2 / C;
+    const long f = blockIdx.x / tiles_per_frame;
+    const int c0 = (int)(blockIdx.x % tiles_per_frame) * C;
+    if (f >= a.nframes) return;
+    const float2* S = a.scratch + f * (long)a.M;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + kFftBlock * i;
+        const int n1 = p / C, col = p % C;
+        lds[fpad(col * a.M1 + n1)] = S[(long)n1 * a.M2 + c0 + col];
+    }
+    __syncthreads();
+    tile_fft<false>(lds, a.M1, a.radixB, a.npassB, a.tw);
+    // X[k2 + M2 k1] -> collated out[(k + M/2) mod M] * norm ; lanes walk k2 (contiguous)
+    float2* O = a.out + f * (long)a.M;
+    const long half = a.M / 2;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + kFftBlock * i;
+        const int k1 = p / C, col = p % C;
+        const long k = (long)(c0 + col) + (long)a.M2 * k1;
+        long o = k + half;
+        if (o >= a.M) o -= a.M;
+        const float2 x = lds[fpad(col * a.M1 + k1)];
+        O[o] = make_float2(x.x * a.norm, x.y * a.norm);
+    }
+}
+
+void radix_plan(int M, int* radix, int* npass) {
+    int n = 0;
+    while (M > 1) {
+        const int r = M >= 16 ? 16 : M;
+        // prefer balanced last stage (e.g. 64 = 16*4, 32 = 16*2)
+        radix[n++] = r;
+        M /= r;
+    }
+    *npass = n;
+}
+
+}  // namespace
+
+// ------------------------------ plan / launch -------------------------------------------
+struct FftPlanDev {
+    int M = 0;
+    int M1 = 0, M2 = 0;
+    float norm = 1.f;
+    float2* tw4096 = nullptr;
+    float2* twM = nullptr;
+};
+
+void* fft_plan_create(int M, int* status) {
+    if (M < 2 || (M & (M - 1)) || M > (1 << 20)) {
+        *status = SDRGPU_ERR_UNSUPPORTED;
+        return nullptr;
+    }
+    auto* p = new FftPlanDev();
+    p->M = M;
+    p->norm = 1.0f / sqrtf((float)M);  // f32, like fft.rs:16
+    std::vector<float2> tw(kTile);
+    for (int m = 0; m < kTile; ++m) {
+        const double ang = -2.0 * M_PI * (double)m / kTile;
+        tw[m] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+    }
+    bool ok = hipMalloc(&p->tw4096, kTile * sizeof(float2)) == hipSuccess &&
+              hipMemcpy(p->tw4096, tw.data(), kTile * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess;
+    if (ok && M > kTile) {
+        // M = M1 * M2 with M2 = largest power of two <= sqrt(M) bounded by the tile
+        int l2 = 0;
+        while ((1 << l2) < M) ++l2;
+        p->M2 = 1 << (l2 / 2);
+        p->M1 = M / p->M2;
+        std::vector<float2> twm(M);
+        for (int m = 0; m < M; ++m) {
+            const double ang = -2.0 * M_PI * (double)m / M;
+            twm[m] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+        }
+        ok = hipMalloc(&p->twM, (size_t)M * sizeof(float2)) == hipSuccess &&
+             hipMemcpy(p->twM, twm.data(), (size_t)M * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (!ok) {
+        fft_plan_destroy(p);
+        *status = SDRGPU_ERR_NOMEM;
+        return nullptr;
+    }
+    *status = SDRGPU_OK;
+    return p;
+}
+
+void fft_plan_destroy(void* plan) {
+    auto* p = static_cast<FftPlanDev*>(plan);
+    if (!p) return;
+    if (p->tw4096) (void)hipFree(p->tw4096);
+    if (p->twM) (void)hipFree(p->twM);
+    delete p;
+}
+
+int fft_plan_size(void* plan) { return static_cast<FftPlanDev*>(plan)->M; }
+
+size_t fft_scratch_frames(void* plan) {
+    auto* p = static_cast<FftPlanDev*>(plan);
+    if (p->M <= kTile) return 0;
+    // keep the slab around 64 MiB so pass B reads it from the MALL
+    const size_t per = (size_t)p->M * sizeof(float2);
+    return std::max<size_t>(1, (64u << 20) / per);
+}
+
+int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
+               size_t scratch_frames, hipStream_t s) {
+    auto* p = static_cast<FftPlanDev*>(plan);
+    FrameSrc src;
+    src.mode = fr.mode;
+    src.in = fr.in;
+    src.in_real = fr.in_real;
+    src.n_in = fr.n_in;
+    src.hist = fr.hist;
+    src.H = fr.H;
+    src.first_end = fr.first_end;
+    src.hop = fr.hop;
+    if (fr.nframes <= 0) return SDRGPU_OK;
+    if (p->M <= kTile) {
+        TileArgs a{};
+        a.src = src;
+        a.nframes = fr.nframes;
+        a.M = p->M;
+        radix_plan(p->M, a.radix, &a.npass);
+        a.tw = p->tw4096;
+        a.norm = p->norm;
+        a.store_mode = store_mode;
+        a.out = out;
+        const long fpt = kTile / p->M;
+        const long nblk = (fr.nframes + fpt - 1) / fpt;
+        hipLaunchKernelGGL(fft_tile_kernel, dim3((unsigned)nblk), dim3(kFftBlock), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+        return SDRGPU_OK;
+    }
+    if (store_mode != 0 || !scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
+    FourArgs a{};
+    a.M = p->M;
+    a.M1 = p->M1;
+    a.M2 = p->M2;
+    radix_plan(p->M2, a.radixA, &a.npassA);
+    radix_plan(p->M1, a.radixB, &a.npassB);
+    a.tw = p->tw4096;
+    a.twM = p->twM;
+    a.norm = p->norm;
+    a.scratch = scratch;
+    for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
+        const long nf = std::min((long)scratch_frames, fr.nframes - f0);
+        a.src = src;
+        if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
+        else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
+        a.nframes = nf;
+        a.out = out + f0 * (long)p->M;
+        const long ga = nf * (a.M1 / (kTile / a.M2));
+        const long gb = nf * (a.M2 / (kTile / a.M1));
+        hipLaunchKernelGGL(fft4_pass_a, dim3((unsigned)ga), dim3(kFftBlock), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+        hipLaunchKernelGGL(fft4_pass_b, dim3((unsigned)gb), dim3(kFftBlock), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+    }
+    return SDRGPU_OK;
+}
+
+// history carry for the STFT stream: hist_next[j] = stream sample (n_in - H + j)
+__global__ void stft_carry_kernel(const float2* in, long n_in, const float2* hist, float2* hist_next,
+                                  long H) {
+    for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < H; j += (long)gridDim.x * blockDim.x) {
+        const long g = n_in - H + j;
+        hist_next[j] = g >= 0 ? in[g] : hist[g + H];
+    }
+}
+
+int stft_carry_launch(const float2* in, long n_in, const float2* hist, float2* hist_next, long H,
+                      hipStream_t s) {
+    if (H <= 0) return SDRGPU_OK;
+    const long nb = std::min<long>((H + 255) / 256, 1024);
+    hipLaunchKernelGGL(stft_carry_kernel, dim3((unsigned)nb), dim3(256), 0, s, in, n_in, hist, hist_next, H);
+    SDRGPU_LAUNCH_CHECK();
+    return SDRGPU_OK;
+}
+
+}  // namespace sdrgpu

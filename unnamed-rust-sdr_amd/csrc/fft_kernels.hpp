@@ -1,0 +1,31 @@
+// fft_kernels.hpp -- internal launch interface of the FFT / STFT kernels.
+#pragma once
+
+#include "common.hpp"
+
+namespace sdrgpu {
+
+// Frame source description (see fft.hip FrameSrc).
+struct FftFrames {
+    int mode;              // 0 contiguous c64 frames, 1 STFT frames from a stream, 2 real frames
+    const float2* in;
+    const float* in_real;
+    long n_in;             // stream samples in this call (mode 1)
+    const float2* hist;    // H previous stream samples (mode 1)
+    long H;
+    long first_end;        // local stream index (exclusive) where frame 0 ends (mode 1)
+    long hop;
+    long nframes;
+};
+
+void* fft_plan_create(int M, int* status);
+void fft_plan_destroy(void* plan);
+int fft_plan_size(void* plan);
+size_t fft_scratch_frames(void* plan);  // 0 if no scratch is needed
+// store_mode 0: collated fft (fft.rs:14-26); 1: rfft upper half (fft.rs:35)
+int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
+               size_t scratch_frames, hipStream_t s);
+int stft_carry_launch(const float2* in, long n_in, const float2* hist, float2* hist_next, long H,
+                      hipStream_t s);
+
+}  // namespace sdrgpu

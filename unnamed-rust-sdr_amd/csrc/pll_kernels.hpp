@@ -1,0 +1,29 @@
+// pll_kernels.hpp -- internal launch interface of the batched PLL kernel.
+#pragma once
+
+#include "common.hpp"
+
+namespace sdrgpu {
+
+struct PllDevParams {
+    long nch;
+    float rate;       // Pll::rate (pll.rs:50)
+    float reference;  // reference / rate (pll.rs:51)
+    float gain;       // pll.rs:52
+    float loopc[5], outc[5], lockc[5];  // b0 b1 b2 na1 na2 (biquad.rs:25-38)
+    int loop_ident, out_ident, lock_ident;
+};
+
+// Per-channel state (Pll fields nphase/value + three biquad states), 20 floats.
+struct PllChannelState {
+    float nphase, vr, vi;
+    float lx1r, lx1i, lx2r, lx2i, ly1r, ly1i, ly2r, ly2i;  // loop filter (complex)
+    float ox1, ox2, oy1, oy2;                               // output filter
+    float kx1, kx2, ky1, ky2;                               // lock filter
+    float pad;
+};
+
+int pll_launch(const PllDevParams& p, const float2* in, long ld_in, long n, float* out,
+               uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s);
+
+}  // namespace sdrgpu
