@@ -1,0 +1,67 @@
+/* Host validation of unnamed-rust-sdr_amd/csrc/libm_glibc.h against this machine's glibc:
+ * sinf/cosf exhaustively over all floats with |x| < LIMIT (both signs), atan2f on N random
+ * (y, x) pairs drawn from four distributions.  Exit code = 0 iff bit-exact everywhere. */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "libm_glibc.h"
+
+typedef struct { uint32_t lo, hi; uint64_t seed; long n, mis; } job;
+
+static void* run_trig(void* a) {
+    job* j = (job*)a;
+    for (uint32_t u = j->lo; u < j->hi; ++u)
+        for (int sg = 0; sg < 2; ++sg) {
+            float x = sdr_asfloat(u | (sg ? 0x80000000u : 0u));
+            if (sdr_asuint(sinf(x)) != sdr_asuint(sdr_sinf(x))) j->mis++;
+            if (sdr_asuint(cosf(x)) != sdr_asuint(sdr_cosf(x))) j->mis++;
+        }
+    return 0;
+}
+
+static inline uint64_t xs(uint64_t* s) { uint64_t x = *s; x ^= x << 13; x ^= x >> 7; x ^= x << 17; return *s = x; }
+
+static void* run_atan2(void* a) {
+    job* j = (job*)a;
+    uint64_t s = j->seed;
+    for (long i = 0; i < j->n; ++i) {
+        uint64_t r = xs(&s);
+        float y, x;
+        switch (r & 3) {
+        case 0: y = sdr_asfloat((uint32_t)(r >> 8)); x = sdr_asfloat((uint32_t)(xs(&s) >> 8)); break;
+        case 1: y = (float)((int32_t)(r >> 32)) / 2147483648.0f; x = (float)((int32_t)(xs(&s) >> 32)) / 2147483648.0f; break;
+        case 2: y = (float)((r >> 40) & 0xffffff) / 16777216.0f * ((r & 8) ? -1e-3f : 1e-3f);
+                x = (float)((int32_t)(xs(&s) >> 32)) / 2147483648.0f; break;
+        default: y = (float)((int32_t)(r >> 32)) / 2147483648.0f * 4;
+                 x = y * (1.0f + ((float)((int32_t)(xs(&s) >> 40)) / 8388608.0f) * 1e-3f); break;
+        }
+        float a1 = atan2f(y, x), a2 = sdr_atan2f(y, x);
+        if (sdr_asuint(a1) != sdr_asuint(a2) && !(isnan(a1) && isnan(a2))) j->mis++;
+    }
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    float limit = argc > 1 ? (float)atof(argv[1]) : 120.0f;
+    long npairs = argc > 2 ? atol(argv[2]) : 100000000L;
+    const int T = 8;
+    pthread_t th[8];
+    job jb[8];
+    uint32_t top = sdr_asuint(limit);
+    long mt = 0, ma = 0;
+    for (int t = 0; t < T; ++t) {
+        jb[t].lo = (uint32_t)((uint64_t)top * t / T); jb[t].hi = (uint32_t)((uint64_t)top * (t + 1) / T);
+        jb[t].mis = 0; pthread_create(&th[t], 0, run_trig, &jb[t]);
+    }
+    for (int t = 0; t < T; ++t) { pthread_join(th[t], 0); mt += jb[t].mis; }
+    for (int t = 0; t < T; ++t) {
+        jb[t].seed = 0x9E3779B97F4A7C15ull * (t + 1); jb[t].n = npairs / T; jb[t].mis = 0;
+        pthread_create(&th[t], 0, run_atan2, &jb[t]);
+    }
+    for (int t = 0; t < T; ++t) { pthread_join(th[t], 0); ma += jb[t].mis; }
+    printf("sinf/cosf |x|<%g: %ld mismatches; atan2f %ld pairs: %ld mismatches\n", limit, mt, npairs, ma);
+    return (mt || ma) ? 1 : 0;
+}

@@ -1,8 +1,10 @@
 """GPU parity: batched PLL FM demod (Pll::apply, src/filter/pll.rs:70-85) vs the oracle.
 
-The loop is a nonlinear recurrence evaluated with libm transcendentals; GPU ocml and host
-glibc differ by a few ulp per call, so parity is judged on outputs (1e-5 of RMS over the
-whole block, None -> 0.0) and on the lock mask (< 0.1 % flips), SURVEY.md 8c."""
+The loop is a chaotic nonlinear recurrence on noisy input (a 1-ulp change in one sample
+moves the next cycle slip), so the GPU kernel restates the reference arithmetic exactly
+(no contraction, reference operation order, glibc-identical sinf/cosf/atan2f -- see
+csrc/libm_glibc.h and tests/test_libm_restatement.py).  Parity is therefore BIT-EXACT:
+outputs (None -> 0.0, src/main.rs:49) and lock masks equal the oracle's."""
 import numpy as np
 import pytest
 
@@ -38,12 +40,11 @@ def oracle_params(oracle, ref=0.0, gain=0.035, loopf=(1, 80000.0, 0.7), outf=(0,
 
 
 def check(out, lk, ref_out, ref_lk, what):
-    flips = np.mean(out.astype(bool) != ref_lk.astype(bool)) if out.size else 0
-    mism = np.mean(lk != ref_lk)
-    assert mism <= 1e-3, f"{what}: lock mismatch {mism:.2e}"
-    both = (lk == 1) & (ref_lk == 1)
-    assert_parity(out[both], ref_out[both], what=what)
-    _ = flips
+    assert np.array_equal(lk, ref_lk), f"{what}: lock mask differs in {np.sum(lk != ref_lk)} samples"
+    if not np.array_equal(out, ref_out):
+        bad = np.argwhere(out != ref_out)
+        raise AssertionError(f"{what}: {len(bad)} outputs differ, first at {bad[0]}")
+    assert_parity(out, ref_out, what=what)
 
 
 def test_pll_fm_batch_parity(sdr, oracle):

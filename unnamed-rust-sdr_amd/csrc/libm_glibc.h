@@ -1,0 +1,242 @@
+/*
+ * libm_glibc.h -- bit-exact restatements of the glibc 2.35 (x86-64) sinf, cosf and atan2f
+ * that the reference calls through Rust std (f32::sin/cos -> sinf/cosf, Complex::arg ->
+ * f32::atan2 -> atan2f; reference src/filter/pll.rs:72,76).
+ *
+ * Why: the reference PLL (pll.rs:70-85) is a chaotic recurrence on noisy input -- a 1-ulp
+ * difference in any sample's sin/cos/atan2 shifts the next cycle slip and the outputs
+ * diverge (measured: FMA vs no-FMA builds of the same restatement differ by 3 % L2).  The
+ * only way to reproduce the reference's outputs is to reproduce its libm bit for bit.
+ *
+ *  - sinf/cosf: glibc sysdeps/ieee754/flt-32 s_sinf.c / s_cosf.c with sincosf.h (double
+ *    evaluation, single-step range reduction for |x| < 120), table __sincosf_table read
+ *    from the system libm binary.  x86-64 glibc dispatches to an FMA build on CPUs with
+ *    FMA (every `a + b*c` contracted); SDR_LIBM_FMA selects that variant.
+ *  - atan2f: fdlibm-derived e_atan2f.c / s_atanf.c (pure f32, not contracted on x86-64).
+ *
+ * The file compiles as C (gcc, for the host validation in tests/) and as HIP device code
+ * (hipcc).  Explicit fma()/fmaf() only where the original contracts; everything else must
+ * be compiled with contraction OFF (-ffp-contract=off).  Validated exhaustively over
+ * |x| < 120 (sinf/cosf) and on random/targeted inputs (atan2f) by
+ * tests/test_libm_restatement.py.
+ */
+#ifndef SDR_LIBM_GLIBC_H
+#define SDR_LIBM_GLIBC_H
+
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
+#define SDR_LIBM_FN __host__ __device__ static inline
+#else
+#include <math.h>
+#define SDR_LIBM_FN static inline
+#endif
+
+#ifndef SDR_LIBM_FMA
+#define SDR_LIBM_FMA 1
+#endif
+
+#if SDR_LIBM_FMA
+#define SDR_MAD(a, b, c) fma((a), (b), (c)) /* c + a*b, contracted */
+#else
+#define SDR_MAD(a, b, c) ((c) + (a) * (b))
+#endif
+
+SDR_LIBM_FN uint32_t sdr_asuint(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+SDR_LIBM_FN float sdr_asfloat(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+/* __sincosf_table[2] (glibc sysdeps/ieee754/flt-32/sincosf_data.c), field order
+ * sign[4], hpi_inv (2/pi * 2^24), hpi, c0, c1, s1, c2, s2, c3, s3, c4. */
+#define SDR_HPI_INV 0x1.45f306dc9c883p+23
+#define SDR_HPI 0x1.921fb54442d18p+0
+#define SDR_C1 -0x1.ffffffd0c621cp-2
+#define SDR_S1 -0x1.555545995a603p-3
+#define SDR_C2 0x1.55553e1068f19p-5
+#define SDR_S2 0x1.1107605230bc4p-7
+#define SDR_C3 -0x1.6c087e89a359dp-10
+#define SDR_S3 -0x1.994eb3774cf24p-13
+#define SDR_C4 0x1.99343027bf8c3p-16
+
+SDR_LIBM_FN uint32_t sdr_abstop12(float x) { return (sdr_asuint(x) >> 20) & 0x7ff; }
+
+/* sinf_poly (sincosf.h): n even -> sine polynomial, odd -> cosine polynomial; neg selects
+ * table[1] (cosine coefficients negated). */
+SDR_LIBM_FN float sdr_sinf_poly(double x, double x2, int n, int neg) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = SDR_MAD(x2, SDR_S3, SDR_S2);
+        double x7 = x3 * x2;
+        double s = SDR_MAD(x3, SDR_S1, x);
+        return (float)SDR_MAD(x7, s1, s);
+    } else {
+        const double c0 = neg ? -1.0 : 1.0;
+        const double kc1 = neg ? -SDR_C1 : SDR_C1, kc2 = neg ? -SDR_C2 : SDR_C2;
+        const double kc3 = neg ? -SDR_C3 : SDR_C3, kc4 = neg ? -SDR_C4 : SDR_C4;
+        double x4 = x2 * x2;
+        double c2 = SDR_MAD(x2, kc4, kc3);
+        double c1 = SDR_MAD(x2, kc1, c0);
+        double x6 = x4 * x2;
+        double c = SDR_MAD(x4, kc2, c1);
+        return (float)SDR_MAD(x6, c2, c);
+    }
+}
+
+/* reduce_fast, !TOINT_INTRINSICS form (x86-64): quadrant in bits 24..31 of r. */
+SDR_LIBM_FN double sdr_reduce_fast(double x, int* np) {
+    double r = x * SDR_HPI_INV;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+#if SDR_LIBM_FMA
+    return fma(-(double)n, SDR_HPI, x);
+#else
+    return x - n * SDR_HPI;
+#endif
+}
+
+/* sinf for |y| < 120 (the PLL phase is 2 pi * fract(.) so |y| < 2 pi). */
+SDR_LIBM_FN float sdr_sinf(float y) {
+    double x = y;
+    if (sdr_abstop12(y) < 0x3f4 /* abstop12(pio4f) */) {
+        double s = x * x;
+        if (sdr_abstop12(y) < 0x398 /* abstop12(0x1p-12f) */) return y;
+        return sdr_sinf_poly(x, s, 0, 0);
+    }
+    int n;
+    x = sdr_reduce_fast(x, &n);
+    const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0; /* sign[n & 3] */
+    return sdr_sinf_poly(x * s, x * x, n, (n & 2) != 0);
+}
+
+SDR_LIBM_FN float sdr_cosf(float y) {
+    double x = y;
+    if (sdr_abstop12(y) < 0x3f4) {
+        double x2 = x * x;
+        if (sdr_abstop12(y) < 0x398) return 1.0f;
+        return sdr_sinf_poly(x, x2, 1, 0);
+    }
+    int n;
+    x = sdr_reduce_fast(x, &n);
+    const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+    return sdr_sinf_poly(x * s, x * x, n ^ 1, (n & 2) != 0);
+}
+
+/* ---- fdlibm atanf (glibc sysdeps/ieee754/flt-32/s_atanf.c) ---- */
+SDR_LIBM_FN float sdr_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f,
+                             1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f,
+                             7.5497894159e-08f};
+    const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+                aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+                aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+                aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+    const float one = 1.0f, huge = 1.0e30f;
+    float w, s1, s2, z;
+    int32_t ix, hx, id;
+    hx = (int32_t)sdr_asuint(x);
+    ix = hx & 0x7fffffff;
+    if (ix >= 0x4c000000) { /* |x| >= 2^25 */
+        if (ix > 0x7f800000) return x + x; /* NaN */
+        if (hx > 0) return atanhi[3] + atanlo[3];
+        return -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) { /* |x| < 0.4375 */
+        if (ix < 0x31000000) { /* |x| < 2^-29 */
+            if (huge + x > one) return x;
+        }
+        id = -1;
+    } else {
+        x = sdr_asfloat(sdr_asuint(x) & 0x7fffffffu); /* fabsf */
+        if (ix < 0x3f980000) {       /* |x| < 1.1875 */
+            if (ix < 0x3f300000) {   /* 7/16 <= |x| < 11/16 */
+                id = 0;
+                x = ((float)2.0 * x - one) / ((float)2.0 + x);
+            } else { /* 11/16 <= |x| < 19/16 */
+                id = 1;
+                x = (x - one) / (x + one);
+            }
+        } else {
+            if (ix < 0x401c0000) { /* |x| < 2.4375 */
+                id = 2;
+                x = (x - (float)1.5) / (one + (float)1.5 * x);
+            } else { /* 2.4375 <= |x| < 2^66 */
+                id = 3;
+                x = -(float)1.0 / x;
+            }
+        }
+    }
+    z = x * x;
+    w = z * z;
+    s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return (hx < 0) ? -z : z;
+}
+
+/* ---- fdlibm atan2f (glibc sysdeps/ieee754/flt-32/e_atan2f.c) ---- */
+SDR_LIBM_FN float sdr_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, zero = 0.0f;
+    const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f;
+    const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    float z;
+    int32_t k, m, hx, hy, ix, iy;
+    hx = (int32_t)sdr_asuint(x);
+    ix = hx & 0x7fffffff;
+    hy = (int32_t)sdr_asuint(y);
+    iy = hy & 0x7fffffff;
+    if ((ix > 0x7f800000) || (iy > 0x7f800000)) return x + y; /* NaN */
+    if (hx == 0x3f800000) return sdr_atanf(y);                 /* x = 1.0 */
+    m = ((hy >> 31) & 1) | ((hx >> 30) & 2);                   /* 2*sign(x)+sign(y) */
+    if (iy == 0) {
+        switch (m) {
+        case 0:
+        case 1: return y;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            switch (m) {
+            case 0: return pi_o_4 + tiny;
+            case 1: return -pi_o_4 - tiny;
+            case 2: return (float)3.0 * pi_o_4 + tiny;
+            default: return (float)-3.0 * pi_o_4 - tiny;
+            }
+        } else {
+            switch (m) {
+            case 0: return zero;
+            case 1: return -zero;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+            }
+        }
+    }
+    if (iy == 0x7f800000) return (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    k = (iy - ix) >> 23;
+    if (k > 60) z = pi_o_2 + (float)0.5 * pi_lo; /* |y/x| > 2^60 */
+    else if (hx < 0 && k < -60) z = 0.0f;        /* |y|/x < -2^60 */
+    else {
+        const float q = y / x;
+        z = sdr_atanf(sdr_asfloat(sdr_asuint(q) & 0x7fffffffu));
+    }
+    switch (m) {
+    case 0: return z;
+    case 1: return sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}
+
+#endif /* SDR_LIBM_GLIBC_H */

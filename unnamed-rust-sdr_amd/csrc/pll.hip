@@ -7,15 +7,19 @@
 //   -> Some(out) if locked > 0.01 else None   (None written as 0.0, src/main.rs:49)
 //
 // The recurrence is serial and nonlinear (atan2 -> NCO -> sin/cos each sample), so it is
-// latency-bound, not HBM- or FLOP-bound: the loop-carried chain is kept as
-// short as the arithmetic allows -- each biquad's terms that only depend on past state are
-// summed before the new input arrives, so only one FMA per filter sits on the chain -- and
-// the next 8 samples of every lane are in flight while the current 8 are processed.
-// Accurate ocml atan2f / sincosf are used (never the __sinf family) so the loop tracks the
-// reference's glibc libm within a few ulp per sample.
+// latency-bound, not HBM- or FLOP-bound; the next 8 samples of every lane
+// are in flight while the current 8 are processed.
+//
+// Bit-exact by construction: on noisy input the reference loop is chaotic (a 1-ulp change
+// in one sample moves the next cycle slip; FMA vs no-FMA builds of the same code differ by
+// 3 % L2), so this kernel reproduces the reference arithmetic exactly: this file is built
+// with -ffp-contract=off, every operation is written in the reference's order (num-complex
+// Mul, Biquad::apply's `0 + v*b0 + x1*b1 + ...`), and sin/cos/atan2 are the bit-exact
+// restatements of the glibc functions Rust std calls (libm_glibc.h).
 #include <algorithm>
 
 #include "common.hpp"
+#include "libm_glibc.h"
 #include "pll_kernels.hpp"
 
 namespace sdrgpu {
@@ -29,12 +33,15 @@ struct Bq {
     float b0, b1, b2, na1, na2;
 };
 
+// Biquad::apply on f32 (biquad.rs:43-56), reference order, no contraction.
 __device__ __forceinline__ float bq_real(const Bq& c, float x, float& x1, float& x2, float& y1,
                                          float& y2) {
-    // reference order: b0 x + b1 x1 + b2 x2 + na1 y1 + na2 y2 (biquad.rs:44-49); the past-
-    // state part is formed first so the new input enters with a single FMA.
-    const float pre = fmaf(c.na1, y1, fmaf(c.b2, x2, fmaf(c.na2, y2, c.b1 * x1)));
-    const float out = fmaf(c.b0, x, pre);
+    float out = 0.0f;
+    out += x * c.b0;
+    out += x1 * c.b1;
+    out += x2 * c.b2;
+    out += y1 * c.na1;
+    out += y2 * c.na2;
     x2 = x1;
     x1 = x;
     y2 = y1;
@@ -84,26 +91,31 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
             const float2 v = cur[k];
-            // c = value * conj(self.value)  (pll.rs:71; num-complex Mul)
-            const float cr = v.x * s.vr - v.y * (-s.vi);
-            const float ci = v.x * (-s.vi) + v.y * s.vr;
+            // c = value * conj(self.value)  (pll.rs:71; num-complex 0.2 Mul)
+            const float cjr = s.vr, cji = -s.vi;
+            const float cr = v.x * cjr - v.y * cji;
+            const float ci = v.x * cji + v.y * cjr;
             float lr = cr, li = ci;
             if (!p.loop_ident) {
-                const float pr = fmaf(L.na1, s.ly1r, fmaf(L.b2, s.lx2r, fmaf(L.na2, s.ly2r, L.b1 * s.lx1r)));
-                const float pi = fmaf(L.na1, s.ly1i, fmaf(L.b2, s.lx2i, fmaf(L.na2, s.ly2i, L.b1 * s.lx1i)));
-                lr = fmaf(L.b0, cr, pr);
-                li = fmaf(L.b0, ci, pi);
-                s.lx2r = s.lx1r; s.lx1r = cr; s.ly2r = s.ly1r; s.ly1r = lr;
-                s.lx2i = s.lx1i; s.lx1i = ci; s.ly2i = s.ly1i; s.ly1i = li;
+                // Biquad<f32, Complex<f32>>::apply: Convolve::accumulate = out += a * c
+                float orr = 0.0f, oi = 0.0f;
+                orr += cr * L.b0;      oi += ci * L.b0;
+                orr += s.lx1r * L.b1;  oi += s.lx1i * L.b1;
+                orr += s.lx2r * L.b2;  oi += s.lx2i * L.b2;
+                orr += s.ly1r * L.na1; oi += s.ly1i * L.na1;
+                orr += s.ly2r * L.na2; oi += s.ly2i * L.na2;
+                s.lx2r = s.lx1r; s.lx1r = cr; s.ly2r = s.ly1r; s.ly1r = orr;
+                s.lx2i = s.lx1i; s.lx1i = ci; s.ly2i = s.ly1i; s.ly1i = oi;
+                lr = orr;
+                li = oi;
             }
-            const float phasedif = atan2f(li, lr) * p.gain;           // :72 arg()
+            const float phasedif = sdr_atan2f(li, lr) * p.gain;       // :72 arg() * gain
             float nph = s.nphase + (p.reference + phasedif);           // :73
             nph = nph - truncf(nph);                                   // :74 fract()
             s.nphase = nph;
-            float sn, cs;
-            sincosf(kTwoPi * nph, &sn, &cs);                           // :75-76 from_polar
-            s.vr = cs;
-            s.vi = sn;
+            const float phase = kTwoPi * nph;                          // :75
+            s.vr = 1.0f * sdr_cosf(phase);                             // :76 from_polar
+            s.vi = 1.0f * sdr_sinf(phase);
             const float lockv = p.lock_ident ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
             const float o = p.out_ident ? phasedif * p.rate
                                         : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
