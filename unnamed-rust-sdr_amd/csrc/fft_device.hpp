@@ -126,17 +126,27 @@ template <bool INV> struct Dft<16, INV> {
     }
 };
 
+// v[r] *= w^r for r = 1..R-1 with a log-depth power tree (w^2 = w*w, w^3 = w^2*w,
+// w^4 = w^2*w^2, ...): at most log2(R) dependent complex multiplies instead of R-2.
+template <int R>
+__device__ __forceinline__ void twiddle_tree(float2* v, float2 w) {
+    float2 p[R];
+    p[1] = w;
+#pragma unroll
+    for (int r = 2; r < R; ++r) {
+        const int a = (r & (r - 1)) ? (r & (r - 1)) : r / 2;  // r with its lowest set bit cleared, or r/2
+        p[r] = cmul(p[a], p[r - a]);
+    }
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], p[r]);
+}
+
 // v[r] *= w^r, r = 1..R-1, with w = tw[m] (forward table) conjugated for the inverse.
 template <int R, bool INV>
 __device__ __forceinline__ void twiddle(float2* v, const float2* __restrict__ tw, int m) {
     float2 w = tw[m];
     if (INV) w.y = -w.y;
-    float2 wr = w;
-#pragma unroll
-    for (int r = 1; r < R; ++r) {
-        v[r] = cmul(v[r], wr);
-        if (r + 1 < R) wr = cmul(wr, w);
-    }
+    twiddle_tree<R>(v, w);
 }
 
 }  // namespace fftd

@@ -234,8 +234,8 @@ __device__ __forceinline__ void os2_load(float2 (&v)[16], const float2* __restri
     }
 }
 
-template <int D>
-__global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long nblk) {
+template <int D, bool PF, int W>
+__global__ __launch_bounds__(kOsBlock, W) void fir_os2_kernel(OsParams p, long nblk) {
     constexpr int L = kOsPoints / D;
     constexpr int R3 = L / 256;
     constexpr int LP = L + L / 16 + 4;
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long n
     long q = blockIdx.x;
     const long hop = (long)p.M * D;
     long base = p.i0 + (q * p.M + p.M - L) * (long)D - (D - 1);
-    if (q < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + t0);
+    if (PF && q < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + t0);
 
 #pragma unroll 1
     for (; q < nblk; q += gridDim.x, base += hop * gridDim.x) {
@@ -289,7 +289,8 @@ __global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long n
         asm volatile("" : "+v"(wi[0].x), "+v"(wi[0].y), "+v"(wi[1].x), "+v"(wi[1].y),
                           "+v"(wi[2].x), "+v"(wi[2].y), "+v"(wi[3].x), "+v"(wi[3].y));
 
-        // ---- P1: radix-16 on the prefetched samples ----
+        // ---- P1: radix-16 on the (prefetched) samples ----
+        if (!PF) os2_load<D>(v, in, hist, p.n_in, K, base + t);
         Dft<16, false>::run(v);
         {
             const int b = D - 1 - (t % D), j = t / D;
@@ -306,12 +307,7 @@ __global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long n
             float2* rd = lds + b * LP + opad(j);
 #pragma unroll
             for (int r = 0; r < 16; ++r) u[r] = rd[ps(NB) * r];
-            float2 wr = w2;
-#pragma unroll
-            for (int r = 1; r < 16; ++r) {
-                u[r] = cmul(u[r], wr);
-                if (r < 15) wr = cmul(wr, w2);
-            }
+            twiddle_tree<16>(u, w2);
             Dft<16, false>::run(u);
             __syncthreads();
             float2* wt = lds + b * LP + opad((j >> 4) * 256 + (j & 15));
@@ -332,12 +328,7 @@ __global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long n
                 float2 w[R3];
 #pragma unroll
                 for (int r = 0; r < R3; ++r) w[r] = rd0[b * LP + 272 * r];
-                float2 wr = w3;
-#pragma unroll
-                for (int r = 1; r < R3; ++r) {
-                    w[r] = cmul(w[r], wr);
-                    if (r + 1 < R3) wr = cmul(wr, w3);
-                }
+                if (R3 > 1) twiddle_tree<R3>(w, w3);
                 Dft<R3, false>::run(w);
 #pragma unroll
                 for (int r = 0; r < R3; ++r) {
@@ -348,7 +339,7 @@ __global__ __launch_bounds__(kOsBlock, 3) void fir_os2_kernel(OsParams p, long n
             }
         }
         // ---- prefetch the next block: flies under I1..I5 (no VMEM loads there) ----
-        if (q + gridDim.x < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + hop * gridDim.x + t);
+        if (PF && q + gridDim.x < nblk) os2_load<D>(v, in, hist, p.n_in, K, base + hop * gridDim.x + t);
         __syncthreads();
 
         // ---- I1: inverse radix-R3, Ns = 1 ----
@@ -516,20 +507,26 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
     p.ld_out = fp.ld_out;
     const long nblk = fp.n_out > 0 ? ceil_div(fp.n_out, st->M) : 1;
     dim3 grid((unsigned)nblk, (unsigned)fp.nch);
-    // persistent grid for the pipelined v2 kernel: ~3 workgroups per CU in total
+    // v2 variants (debug knob SDRGPU_OS_VARIANT): 0 = persistent + prefetch, 3 waves/SIMD
+    // (default); 1 = persistent, no prefetch, 4 waves/SIMD; 2 = v1 (one block per WG).
+    static const char* var_env = getenv("SDRGPU_OS_VARIANT");
     static const char* force_v1 = getenv("SDRGPU_OS_V1");
-    const long per_ch = std::max(1L, std::min(nblk, (256L * 3 + fp.nch - 1) / fp.nch));
+    int variant = var_env ? atoi(var_env) : 0;
+    if (force_v1 && force_v1[0] == '1') variant = 2;
+    const int wgs_per_cu = variant == 1 ? 4 : 3;
+    const long per_ch = std::max(1L, std::min(nblk, (256L * wgs_per_cu + fp.nch - 1) / fp.nch));
     dim3 pgrid((unsigned)per_ch, (unsigned)fp.nch);
-    const bool v2 = !(force_v1 && force_v1[0] == '1');
     switch (st->D) {
     case 1: hipLaunchKernelGGL(fir_os_kernel<1>, grid, dim3(kOsBlock), 0, s, p); break;
     case 2: hipLaunchKernelGGL(fir_os_kernel<2>, grid, dim3(kOsBlock), 0, s, p); break;
     case 4:
-        if (v2) hipLaunchKernelGGL(fir_os2_kernel<4>, pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        if (variant == 0) hipLaunchKernelGGL((fir_os2_kernel<4, true, 3>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 1) hipLaunchKernelGGL((fir_os2_kernel<4, false, 4>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else hipLaunchKernelGGL(fir_os_kernel<4>, grid, dim3(kOsBlock), 0, s, p);
         break;
     case 8:
-        if (v2) hipLaunchKernelGGL(fir_os2_kernel<8>, pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        if (variant == 0) hipLaunchKernelGGL((fir_os2_kernel<8, true, 3>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 1) hipLaunchKernelGGL((fir_os2_kernel<8, false, 4>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else hipLaunchKernelGGL(fir_os_kernel<8>, grid, dim3(kOsBlock), 0, s, p);
         break;
     default: return SDRGPU_ERR_UNSUPPORTED;

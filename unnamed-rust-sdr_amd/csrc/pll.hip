@@ -64,79 +64,73 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
     const Bq K = {p.lockc[0], p.lockc[1], p.lockc[2], p.lockc[3], p.lockc[4]};
     constexpr float kTwoPi = 2.0f * 3.14159265358979323846f;  // 2.0 * f32::consts::PI
 
-    float2 buf[kChunk];
-    long i = 0;
+    // one reference Pll::apply step; returns (output or 0, locked)
+    auto step = [&](float2 v, float& ov, uint8_t& lv) {
+        // c = value * conj(self.value)  (pll.rs:71; num-complex 0.2 Mul)
+        const float cjr = s.vr, cji = -s.vi;
+        const float cr = v.x * cjr - v.y * cji;
+        const float ci = v.x * cji + v.y * cjr;
+        float lr = cr, li = ci;
+        if (!p.loop_ident) {
+            // Biquad<f32, Complex<f32>>::apply: Convolve::accumulate = out += a * c
+            float orr = 0.0f, oi = 0.0f;
+            orr += cr * L.b0;      oi += ci * L.b0;
+            orr += s.lx1r * L.b1;  oi += s.lx1i * L.b1;
+            orr += s.lx2r * L.b2;  oi += s.lx2i * L.b2;
+            orr += s.ly1r * L.na1; oi += s.ly1i * L.na1;
+            orr += s.ly2r * L.na2; oi += s.ly2i * L.na2;
+            s.lx2r = s.lx1r; s.lx1r = cr; s.ly2r = s.ly1r; s.ly1r = orr;
+            s.lx2i = s.lx1i; s.lx1i = ci; s.ly2i = s.ly1i; s.ly1i = oi;
+            lr = orr;
+            li = oi;
+        }
+        const float phasedif = sdr_atan2f(li, lr) * p.gain;       // :72 arg() * gain
+        float nph = s.nphase + (p.reference + phasedif);           // :73
+        nph = nph - truncf(nph);                                   // :74 fract()
+        s.nphase = nph;
+        const float phase = kTwoPi * nph;                          // :75
+        s.vr = 1.0f * sdr_cosf(phase);                             // :76 from_polar
+        s.vi = 1.0f * sdr_sinf(phase);
+        const float lockv = p.lock_ident ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
+        const float o = p.out_ident ? phasedif * p.rate
+                                    : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
+        const bool lockd = lockv > 0.01f;                          // :80
+        ov = lockd ? o : 0.0f;
+        lv = lockd ? 1 : 0;
+    };
+
+    // full chunks of kChunk samples, the next chunk's loads in flight
     const long nfull = n / kChunk * kChunk;
+    float2 buf[kChunk];
     if (nfull > 0) {
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) buf[k] = x[k];
     }
-    for (; i < n; i += kChunk) {
-        const bool full = i < nfull;
+    for (long i = 0; i < nfull; i += kChunk) {
         float2 cur[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) cur[k] = buf[k];
-        if (!full) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) cur[k] = (i + k < n) ? x[i + k] : make_float2(0.f, 0.f);
-        } else if (i + kChunk < nfull) {
+        if (i + kChunk < nfull) {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) buf[k] = x[i + kChunk + k];  // prefetch
-        } else if (i + kChunk < n) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) buf[k] = make_float2(0.f, 0.f);
         }
         float ov[kChunk];
         uint8_t lv[kChunk];
 #pragma unroll
+        for (int k = 0; k < kChunk; ++k) step(cur[k], ov[k], lv[k]);
+#pragma unroll
         for (int k = 0; k < kChunk; ++k) {
-            const float2 v = cur[k];
-            // c = value * conj(self.value)  (pll.rs:71; num-complex 0.2 Mul)
-            const float cjr = s.vr, cji = -s.vi;
-            const float cr = v.x * cjr - v.y * cji;
-            const float ci = v.x * cji + v.y * cjr;
-            float lr = cr, li = ci;
-            if (!p.loop_ident) {
-                // Biquad<f32, Complex<f32>>::apply: Convolve::accumulate = out += a * c
-                float orr = 0.0f, oi = 0.0f;
-                orr += cr * L.b0;      oi += ci * L.b0;
-                orr += s.lx1r * L.b1;  oi += s.lx1i * L.b1;
-                orr += s.lx2r * L.b2;  oi += s.lx2i * L.b2;
-                orr += s.ly1r * L.na1; oi += s.ly1i * L.na1;
-                orr += s.ly2r * L.na2; oi += s.ly2i * L.na2;
-                s.lx2r = s.lx1r; s.lx1r = cr; s.ly2r = s.ly1r; s.ly1r = orr;
-                s.lx2i = s.lx1i; s.lx1i = ci; s.ly2i = s.ly1i; s.ly1i = oi;
-                lr = orr;
-                li = oi;
-            }
-            const float phasedif = sdr_atan2f(li, lr) * p.gain;       // :72 arg() * gain
-            float nph = s.nphase + (p.reference + phasedif);           // :73
-            nph = nph - truncf(nph);                                   // :74 fract()
-            s.nphase = nph;
-            const float phase = kTwoPi * nph;                          // :75
-            s.vr = 1.0f * sdr_cosf(phase);                             // :76 from_polar
-            s.vi = 1.0f * sdr_sinf(phase);
-            const float lockv = p.lock_ident ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
-            const float o = p.out_ident ? phasedif * p.rate
-                                        : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
-            const bool lockd = lockv > 0.01f;                          // :80
-            ov[k] = lockd ? o : 0.0f;
-            lv[k] = lockd ? 1 : 0;
+            y[i + k] = ov[k];
+            lk[i + k] = lv[k];
         }
-        if (full) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                y[i + k] = ov[k];
-                lk[i + k] = lv[k];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k)
-                if (i + k < n) {
-                    y[i + k] = ov[k];
-                    lk[i + k] = lv[k];
-                }
-        }
+    }
+    // ragged tail: exactly n - nfull more samples (the state must not see padding)
+    for (long i = nfull; i < n; ++i) {
+        float o;
+        uint8_t l;
+        step(x[i], o, l);
+        y[i] = o;
+        lk[i] = l;
     }
     state[ch] = s;
 }
