@@ -82,6 +82,36 @@ def cpu_baseline(taps, seconds):
                       f"Fir(255 taps)+Decimate(4), {el:.1f} s on 1 host core"}
 
 
+def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
+    """Run `warmup` untimed steps, then exactly `steps` timed steps bracketed by a barrier
+    and a device synchronize on both sides; return the MAX elapsed seconds over ranks.
+    `on_step(i, phase)` is called with phase 'begin'/'end' around each timed step (event
+    recording).  Pure host logic: tests/test_dist_cpu.py drives it with gloo ranks."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if on_step:
+            on_step(i, "begin")
+        step()
+        if on_step:
+            on_step(i, "end")
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,7 +137,8 @@ def main():
                             algorithm=algo).design(2.4e6)
     stream = fir.stream()
 
-    # this rank's time shard: a 2^22-sample synthetic pattern (distinct per rank) tiled
+    # This rank's time shard of one long stream: shard r covers stream samples
+    # [r*n, (r+1)*n).  Synthetic data: a 2^22-sample pattern (distinct per rank) tiled.
     pat_n = min(n, 1 << 22)
     pat = synth_iq_pattern(pat_n, seed=1000 + rank)
     x = DeviceBuffer.empty(n, np.complex64, device=local)
@@ -115,36 +146,31 @@ def main():
         x.upload(pat[:min(pat_n, n - off)], offset_bytes=8 * off)
     n_out = n // D
     y = DeviceBuffer.empty(n_out, np.complex64, device=local)
+    if rank > 0:
+        # halo: the 256 stream samples preceding this shard (tail of rank-1's shard) prime
+        # the FIR history, so the sharded outputs equal the unsharded stream's exactly
+        prev = synth_iq_pattern(pat_n, seed=1000 + rank - 1)
+        halo = prev[(n - 256) % pat_n:][:256] if pat_n >= 256 else prev
+        hb = DeviceBuffer.from_numpy(np.ascontiguousarray(halo), device=local)
+        hy = DeviceBuffer.empty(64, np.complex64, device=local)
+        fir.process_dev(hb.ptr, 256, hy.ptr, 64)
     synchronize(local)
 
     def step():
         got = fir.process_dev(x.ptr, n, y.ptr, n_out)
         assert got == n_out, (got, n_out)
 
-    for _ in range(args.warmup):
-        step()
-    fir.sync()
-
     starts = [Event(local) for _ in range(args.steps)]
     ends = [Event(local) for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    synchronize(local)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record(stream)
-        step()
-        ends[i].record(stream)
-    fir.sync()
-    synchronize(local)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    def on_step(i, phase):
+        (starts if phase == "begin" else ends)[i].record(stream)
+
+    def sync():
+        fir.sync()
+        synchronize(local)
+
+    elapsed = timed_region(step, args.steps, args.warmup, sync, dist, on_step)
     kern_ms = float(np.mean([s.elapsed_ms(e) for s, e in zip(starts, ends)]))
     total_samples = n * args.steps * world
     value = total_samples / elapsed / 1e6

@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""bench_configs.py -- measurements for the other BASELINE.json configs.
+
+bench.py is the driver's headline line (configs[1]); this script measures configs[2..4]
+with the same rules (inputs resident in HBM, HIP-event-timed kernels on the handle's
+stream, algorithmic bytes per input sample, a bounded CPU-baseline sample), one JSON line
+per config:
+
+  c3  64k-point STFT, 50 % overlap, 2^28 c64 samples      24 B / input sample, HBM roof
+  c4  255-tap matched filter (FIR bank) + PLL FM demod,    12 B / input sample (+1 lock);
+      1024 channels x 2^20 c64                              PLL = loop-carried latency
+  c5  255-tap FIR bank, channels sharded across GPUs,      16 B / input sample, HBM roof
+      8192 channels x 2^16 c64 (1024 per GPU at 8 GPUs)
+
+Multi-GPU (c5): `python -m torch.distributed.run --nproc-per-node N bench_configs.py
+--config c5`; each rank filters its resident channel shard (weak: 8192/N channels per rank
+... see --c5-weak), and RCCL scatter (root -> ranks) / gather (ranks -> root) of the
+channel blocks is timed separately ("fan-out/gather only", north_star).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "unnamed-rust-sdr_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "all"])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--c3-log2n", type=int, default=28)
+    ap.add_argument("--c4-log2n", type=int, default=20)
+    ap.add_argument("--c4-nch", type=int, default=1024)
+    ap.add_argument("--c5-nch", type=int, default=8192)
+    ap.add_argument("--c5-log2n", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cplx_pattern(n, seed):
+    r = np.random.default_rng(seed)
+    return ((r.standard_normal(n, dtype=np.float32) + 1j * r.standard_normal(n, dtype=np.float32))
+            * 0.3).astype(np.complex64)
+
+
+def fill(buf, n, seed, pat_n=1 << 22):
+    pat = cplx_pattern(min(n, pat_n), seed)
+    for off in range(0, n, len(pat)):
+        buf.upload(pat[:min(len(pat), n - off)], offset_bytes=8 * off)
+
+
+def time_events(step, stream, steps, warmup, sync):
+    from sdrgpu.device import Event
+    for _ in range(warmup):
+        step()
+    sync()
+    ev = [(Event(), Event()) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    sync()
+    wall = (time.perf_counter() - t0) / steps
+    return wall, float(np.mean([a.elapsed_ms(b) for a, b in ev]))
+
+
+def roof(bytes_per_unit, units, ms):
+    gbs = bytes_per_unit * units / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_GBS, 4), "kernel_ms": round(ms, 4)}
+
+
+# ------------------------------------------------------------------------------ c3
+def bench_c3(args):
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    N, hop = 65536, 32768
+    n = 1 << args.c3_log2n
+    st = sdrgpu.fft.Stft(N, hop)
+    x = DeviceBuffer.empty(n)
+    fill(x, n, 3)
+    nf = st.output_len(n)
+    y = DeviceBuffer.empty(nf * N)
+
+    def step():
+        st.reset()
+        assert st.process_dev(x.ptr, n, y.ptr, nf) == nf
+
+    wall, ms = time_events(step, st.stream(), args.steps, args.warmup, lambda: (st.sync(), synchronize()))
+    res = {"config": "c3: 64k-point STFT, 50% overlap, fftshift + 1/sqrt(N), 2^28 c64 samples",
+           "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
+           "frames": nf, "roofline": roof(24, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
+    if not args.no_cpu_baseline:
+        xf = cplx_pattern(N, 7)
+        t0, done = time.perf_counter(), 0
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            np.fft.fftshift(np.fft.fft(xf)) / np.float32(np.sqrt(N))
+            done += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(done * hop / el / 1e6, 2), "unit": "complex Msamples/s",
+                               "cores": 1, "kind": "proxy",
+                               "sample": f"{done} NumPy pocketfft 64k frames (proxy for rustfft 3.0), {el:.1f} s"}
+    return res
+
+
+# ------------------------------------------------------------------------------ c4
+def bench_c4(args):
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    f = sdrgpu.filter
+    nch, n = args.c4_nch, 1 << args.c4_log2n
+    rate = 1.8e6
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    bank = f.FirBank(taps, nch, sample_kind=sdrgpu.C64)
+    pll = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
+                      f.BiquadD.LowPass(20000.0, 0.7)).design(rate, nch=nch)
+    pll.set_stream(bank.stream())
+    x = DeviceBuffer.empty(nch * n)
+    fill(x, nch * n, 4)
+    mf = DeviceBuffer.empty(nch * n)
+    out = DeviceBuffer.empty(nch * n, np.float32)
+    lk = DeviceBuffer.empty(nch * n, np.uint8)
+
+    def step():
+        bank.process_dev(x.ptr, n, n, mf.ptr, n)
+        pll.process_dev(mf.ptr, n, n, out.ptr, lk.ptr, n)
+
+    wall, ms = time_events(step, bank.stream(), args.steps, args.warmup, lambda: (bank.sync(), synchronize()))
+    # split: matched filter alone
+    _, ms_fir = time_events(lambda: bank.process_dev(x.ptr, n, n, mf.ptr, n), bank.stream(),
+                            args.steps, 0, lambda: (bank.sync(), synchronize()))
+    units = nch * n
+    res = {"config": f"c4: 255-tap matched filter + PLL FM demod (src/main.rs:41-46), {nch} ch x 2^{args.c4_log2n}",
+           "metric": "complex Msamples/s (input, all channels)", "value": round(units / (ms * 1e-3) / 1e6, 1),
+           "roofline": roof(12, units, ms), "fir_ms": round(ms_fir, 3), "pll_ms": round(ms - ms_fir, 3),
+           "pll_ns_per_sample_chain": round((ms - ms_fir) * 1e6 / n, 2),
+           "note": "PLL is bound by its loop-carried latency (ns per sample per channel chain), not HBM",
+           "wall_ms_per_step": round(wall * 1e3, 3)}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        cores = min(os.cpu_count() or 1, 16)
+        cn, cl = cores, 1 << 14
+        xs = cplx_pattern(cn * cl, 8).reshape(cn, cl)
+        p = pyoracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
+        t0, done = time.perf_counter(), 0
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            m = pyoracle.fir_batch(taps, xs, 1, nthreads=cores)
+            pyoracle.pll_batch(p, m, nthreads=cores)
+            done += cn * cl
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(done / el / 1e6, 2), "unit": "complex Msamples/s",
+                               "cores": cores, "kind": "port",
+                               "sample": f"{done} samples ({cn} ch x 2^14 blocks) oracle FIR+PLL, {el:.1f} s"}
+    return res
+
+
+# ------------------------------------------------------------------------------ c5
+def bench_c5(args):
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    from sdrgpu.shard import Comm, channel_range, unique_id
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    nch_total, n = args.c5_nch, 1 << args.c5_log2n
+    lo, hi = channel_range(nch_total, world, rank)
+    nch = hi - lo
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    bank = sdrgpu.filter.FirBank(taps, nch, sample_kind=sdrgpu.C64, device=local)
+    x = DeviceBuffer.empty(nch * n, device=local)
+    fill(x, nch * n, 50 + rank)
+    y = DeviceBuffer.empty(nch * n, device=local)
+
+    def step():
+        bank.process_dev(x.ptr, n, n, y.ptr, n)
+
+    wall, ms = time_events(step, bank.stream(), args.steps, args.warmup,
+                           lambda: (bank.sync(), synchronize(local)))
+    t = [ms]
+    if dist is not None:
+        import torch
+        tt = torch.tensor([ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = [float(tt.item())]
+    res = {"config": f"c5: 255-tap FIR bank, {nch_total} ch x 2^{args.c5_log2n} c64, {world} GPU(s), "
+                     f"{nch} resident channels per rank",
+           "metric": "complex Msamples/s (input, all ranks)",
+           "value": round(nch_total * n / (t[0] * 1e-3) / 1e6, 1) if world > 1 else round(nch * n / (ms * 1e-3) / 1e6, 1),
+           "roofline_rank0": roof(16, nch * n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
+    if dist is not None and nch_total % world == 0:
+        # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately)
+        ids = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        comm = Comm(local, world, rank, ids[0])
+        blk = nch * n * 8
+        full = DeviceBuffer(blk * world, local) if rank == 0 else None
+        s = bank.stream()
+        from sdrgpu.device import Event
+        e0, e1, e2 = Event(local), Event(local), Event(local)
+        comm.barrier(s)
+        e0.record(s)
+        comm.scatter(full.ptr if full else None, x.ptr, blk, 0, s)
+        e1.record(s)
+        comm.gather(y.ptr, full.ptr if full else None, blk, 0, s)
+        e2.record(s)
+        bank.sync()
+        res["rccl_scatter_ms"] = round(e0.elapsed_ms(e1), 3)
+        res["rccl_gather_ms"] = round(e1.elapsed_ms(e2), 3)
+        res["end_to_end_value"] = round(nch_total * n / ((t[0] + e0.elapsed_ms(e2)) * 1e-3) / 1e6, 1)
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return res if rank == 0 else None
+
+
+def main():
+    args = parse()
+    todo = ["c3", "c4", "c5"] if args.config == "all" else [args.config]
+    for c in todo:
+        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5}[c](args)
+        if r is not None:
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -223,6 +223,28 @@ int sdrgpu_pll_reset(sdrgpu_pll* h);
 int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out);
 void sdrgpu_pll_destroy(sdrgpu_pll* h);
 
+/* =====================================================================================
+ * Multi-GPU channel sharding (configs[4]: channels sharded across the GPUs of one node).
+ * No reference counterpart (the reference is single-process CPU code):
+ * channels are independent, so the only collectives are the fan-out of channel blocks from
+ * a root and the gather of results back -- RCCL over xGMI, one process per GPU.  The
+ * 128-byte unique id is created on rank 0 and shared out of band (e.g. torch.distributed
+ * over gloo).  Byte counts are per rank; buffers are device pointers.
+ * ===================================================================================== */
+typedef struct sdrgpu_comm sdrgpu_comm;
+#define SDRGPU_COMM_ID_BYTES 128
+
+int sdrgpu_comm_unique_id(void* id_out /* SDRGPU_COMM_ID_BYTES */);
+int sdrgpu_comm_init(int device, int nranks, int rank, const void* id, sdrgpu_comm** out);
+/* root's d_send holds nranks consecutive blocks of bytes_per_rank; rank i gets block i */
+int sdrgpu_comm_scatter(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t bytes_per_rank,
+                        int root, void* hip_stream);
+/* rank i's block lands at d_recv + i*bytes_per_rank on root */
+int sdrgpu_comm_gather(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t bytes_per_rank,
+                       int root, void* hip_stream);
+int sdrgpu_comm_barrier(sdrgpu_comm* c, void* hip_stream);
+void sdrgpu_comm_destroy(sdrgpu_comm* c);
+
 #ifdef __cplusplus
 }
 #endif

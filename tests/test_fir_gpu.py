@@ -235,3 +235,20 @@ def test_fir_full_size_c2_properties(sdr, oracle):
     for y1, m in zip(ys, (0, n_out // 2, n_out - (1 << 20))):
         y2 = dy.download(1 << 20, offset_bytes=8 * m)
         assert np.array_equal(y2, 2 * y1)
+
+
+@pytest.mark.parametrize("algo", ["direct", "auto"])
+def test_time_shard_halo_equivalence(sdr, oracle, algo):
+    """Multi-GPU time sharding (bench.py): a shard primed with the 256 preceding samples
+    produces exactly the continuation of the unsharded stream."""
+    rng = np.random.default_rng(21)
+    taps, x = make_case(rng, 1, 0, 255, 80000)
+    whole = fir(sdr, taps, 1, 4, algo).process(x)
+    half = 40000
+    f2 = fir(sdr, taps, 1, 4, algo)
+    f2.process(x[half - 256:half])          # halo priming; its outputs belong to shard 0
+    y2 = f2.process(x[half:])
+    assert y2.shape == whole[half // 4:].shape
+    if algo == "direct":
+        assert np.array_equal(y2, whole[half // 4:])
+    assert_parity(y2, oracle.Fir(taps, 4, sample_kind=1).process(x)[half // 4:])

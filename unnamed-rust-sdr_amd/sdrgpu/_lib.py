@@ -139,6 +139,13 @@ SIGNATURES = [
     ("sdrgpu_pll_reset", c_int, [_H]),
     ("sdrgpu_pll_clone", c_int, [_H, _PH]),
     ("sdrgpu_pll_destroy", None, [_H]),
+    # multi-GPU fan-out / gather (RCCL)
+    ("sdrgpu_comm_unique_id", c_int, [c_void_p]),
+    ("sdrgpu_comm_init", c_int, [c_int, c_int, c_int, c_void_p, _PH]),
+    ("sdrgpu_comm_scatter", c_int, [_H, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    ("sdrgpu_comm_gather", c_int, [_H, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    ("sdrgpu_comm_barrier", c_int, [_H, c_void_p]),
+    ("sdrgpu_comm_destroy", None, [_H]),
 ]
 
 _LIB = None

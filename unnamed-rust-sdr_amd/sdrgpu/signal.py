@@ -1,0 +1,223 @@
+"""Host-side mirror of the reference `Signal` trait (src/signal/mod.rs:13-123) over sdrgpu.
+
+The reference pulls one sample at a time through adapter structs; here a Signal yields
+BLOCKS (numpy arrays) and every GPU-backed stage carries its stream state across blocks,
+so results equal the sample-by-sample reference for any block size.  Combinators keep the
+reference names and argument meaning:
+
+  filter(design)     adapters::Filter (adapters/mod.rs:66-100): FIR taps / filter.Fir
+                     (fir.rs:36-58) or filter.PllDesign (pll.rs:39-61, output Option<f32>
+                     as (value-or-0.0, locked) blocks like src/main.rs:49 unwraps it)
+  decimate(rate)     Decimate (adapters/mod.rs:13-41): wait = round(rate_in / rate), keeps
+                     upstream indices wait-1, 2wait-1, ...; rate() stays the UPSTREAM rate
+                     (the reference quirk, :38-40).  A decimate directly after a FIR filter
+                     is fused into the FIR kernel (only kept outputs are computed).
+  window(duration)   Window (adapters/mod.rs:270-303), cap = round(duration * rate)
+  .decimate(..).map(fft)  the live.rs STFT pattern -> one GPU Stft stage
+  map(f), take(duration), skip(duration), iter(), collect()
+
+Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), impulse
+(sources.rs:223-257).
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterator, Optional
+
+import numpy as np
+
+from . import _lib
+from . import filter as _filter
+from . import fft as _fft
+
+DEFAULT_BLOCK = 1 << 16
+
+
+class Signal:
+    def __init__(self, rate: float, blocks: Callable[[], Iterator[np.ndarray]],
+                 sample_kind: Optional[int] = None, _fir: Optional[dict] = None):
+        self._rate = float(rate)
+        self._blocks = blocks
+        self.sample_kind = sample_kind
+        self._fir = _fir  # pending FIR stage that a following decimate may fuse into
+
+    # ---- Signal::rate / iteration ----
+    def rate(self) -> float:
+        return self._rate
+
+    def blocks(self) -> Iterator[np.ndarray]:
+        return self._blocks()
+
+    def iter(self):
+        for b in self.blocks():
+            yield from b
+
+    def collect(self) -> np.ndarray:
+        bl = [b for b in self.blocks()]
+        return np.concatenate(bl) if bl else np.zeros(0)
+
+    # ---- combinators ----
+    def filter(self, design, block_kind=None) -> "Signal":
+        if isinstance(design, _filter.PllDesign):
+            return self._pll(design)
+        if isinstance(design, (list, tuple, np.ndarray)):
+            design = _filter.Fir(np.asarray(design))
+        if isinstance(design, _filter.Fir):
+            return self._fir_stage(design, 1)
+        raise _lib.SdrGpuError(_lib.ERR_UNSUPPORTED,
+                               f"Signal.filter: {type(design).__name__} is not on the GPU path")
+
+    def _fir_stage(self, fir: "_filter.Fir", decim: int) -> "Signal":
+        up = self
+        sk = self.sample_kind if self.sample_kind is not None else (
+            _lib.C64 if fir.tap_kind == _lib.C64 else _lib.F32)
+
+        def gen():
+            f = fir.with_decim(decim).design(up.rate(), sample_kind=sk)
+            for b in up.blocks():
+                y = f.process(b)
+                if y.size:
+                    yield y
+        return Signal(self._rate, gen, sk, _fir={"up": up, "fir": fir, "decim": decim})
+
+    def _pll(self, design: "_filter.PllDesign") -> "Signal":
+        up = self
+
+        def gen():
+            p = design.design(up.rate())
+            for b in up.blocks():
+                out, locked = p.process(np.asarray(b, np.complex64))
+                yield np.rec.fromarrays([out, locked.astype(bool)], names="value,locked")
+        return Signal(self._rate, gen, None)
+
+    def decimate(self, rate: float) -> "Signal":
+        wait = int(round(self._rate / rate))
+        if wait < 1:
+            raise _lib.SdrGpuError(_lib.ERR_INVALID, "decimate: rate above the input rate")
+        if self._fir is not None and self._fir["decim"] == 1:
+            # Filter(..).decimate(..): fuse -> only kept outputs are computed on the GPU
+            return self._fir["up"]._fir_stage(self._fir["fir"], wait)
+        if getattr(self, "_window", None) is not None:
+            return _WindowDecimate(self, self._window, wait)
+        up = self
+
+        def gen():
+            phase = 0  # samples consumed mod wait
+            for b in up.blocks():
+                first = (wait - 1 - phase) % wait
+                yield b[first::wait]
+                phase = (phase + len(b)) % wait
+        return Signal(self._rate, gen, self.sample_kind)  # Decimate::rate quirk (:38-40)
+
+    def window(self, duration: float) -> "Signal":
+        cap = int(round(duration * self._rate))
+        s = Signal(self._rate, self._blocks, self.sample_kind)
+        s._window = cap
+        return s
+
+    def map(self, fn: Callable) -> "Signal":
+        up = self
+
+        def gen():
+            for b in up.blocks():
+                yield fn(b)
+        return Signal(self._rate, gen, None)
+
+    def take(self, duration: float) -> "Signal":
+        n = int(round(self._rate * duration))
+        up = self
+
+        def gen():
+            left = n
+            for b in up.blocks():
+                if left <= 0:
+                    return
+                yield b[:left]
+                left -= len(b)
+        return Signal(self._rate, gen, self.sample_kind)
+
+    def skip(self, duration: float) -> "Signal":
+        n = int(round(self._rate * duration))
+        up = self
+
+        def gen():
+            left = n
+            for b in up.blocks():
+                if left >= len(b):
+                    left -= len(b)
+                    continue
+                yield b[left:]
+                left = 0
+        return Signal(self._rate, gen, self.sample_kind)
+
+
+class _WindowDecimate(Signal):
+    """window(N).decimate(rate): frames x[(j+1)hop - N .. (j+1)hop) (adapters/mod.rs:277-299).
+    .map(fft) on it runs the GPU STFT; other maps get the raw frames."""
+
+    def __init__(self, up: Signal, cap: int, hop: int):
+        self.up, self.cap, self.hop = up, cap, hop
+
+        def frames():
+            buf = np.zeros(cap, np.complex64)
+            phase = 0
+            for b in up.blocks():
+                for v in b:
+                    buf = np.roll(buf, -1)
+                    buf[-1] = v
+                    phase += 1
+                    if phase == hop:
+                        phase = 0
+                        yield buf.copy()[None, :]
+        super().__init__(up.rate(), frames, None)
+
+    def map(self, fn: Callable) -> Signal:
+        if fn is fft or fn is _fft.fft:
+            up, cap, hop = self.up, self.cap, self.hop
+
+            def gen():
+                s = _fft.Stft(cap, hop)
+                for b in up.blocks():
+                    y = s.process(b)
+                    if y.shape[0]:
+                        yield y
+            return Signal(self._rate, gen, None)
+        return super().map(fn)
+
+
+def fft(frames):
+    """Marker for .map(fft) on window+decimate (the examples/live.rs STFT)."""
+    return np.stack([_fft.fft(f, 1.0)[1] for f in np.atleast_2d(frames)])
+
+
+# ---------------------------------------------------------------- sources
+def from_array(rate: float, x, block: int = DEFAULT_BLOCK) -> Signal:
+    x = np.asarray(x)
+    sk = _lib.C64 if np.iscomplexobj(x) else _lib.F32
+
+    def gen():
+        for i in range(0, len(x), block):
+            yield x[i:i + block]
+    return Signal(rate, gen, sk)
+
+
+def freq(rate: float, f: float, phase: float, n: int, block: int = DEFAULT_BLOCK) -> Signal:
+    """signal::freq (sources.rs:196-221) for n samples (FreqSweep::next arithmetic in f32)."""
+    two_pi = np.float32(2.0) * np.float32(np.pi)
+    dt = np.float32(1.0) / np.float32(rate)
+    ff = np.float32(f)
+    nph = np.float32(phase) / two_pi
+    out = np.empty(n, np.complex64)
+    for i in range(n):
+        nph = np.float32(nph + np.float32(dt * ff))
+        nph = np.float32(nph - np.trunc(nph))
+        ph = np.float32(two_pi * nph)
+        out[i] = complex(np.cos(ph, dtype=np.float32), np.sin(ph, dtype=np.float32))
+    return from_array(rate, out, block)
+
+
+def impulse(rate: float, n: int, complex_: bool = False, block: int = DEFAULT_BLOCK) -> Signal:
+    """signal::impulse (sources.rs:223-257): 1 then zeros (n samples)."""
+    x = np.zeros(n, np.complex64 if complex_ else np.float32)
+    if n:
+        x[0] = 1
+    return from_array(rate, x, block)
