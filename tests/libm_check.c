@@ -16,8 +16,13 @@ static void* run_trig(void* a) {
     for (uint32_t u = j->lo; u < j->hi; ++u)
         for (int sg = 0; sg < 2; ++sg) {
             float x = sdr_asfloat(u | (sg ? 0x80000000u : 0u));
-            if (sdr_asuint(sinf(x)) != sdr_asuint(sdr_sinf(x))) j->mis++;
-            if (sdr_asuint(cosf(x)) != sdr_asuint(sdr_cosf(x))) j->mis++;
+            const float rs = sinf(x), rc = cosf(x);
+            if (sdr_asuint(rs) != sdr_asuint(sdr_sinf(x))) j->mis++;
+            if (sdr_asuint(rc) != sdr_asuint(sdr_cosf(x))) j->mis++;
+            float bs, bc;
+            sdr_sincosf_bf(x, &bs, &bc); /* branch-free GPU form */
+            if (sdr_asuint(rs) != sdr_asuint(bs)) j->mis++;
+            if (sdr_asuint(rc) != sdr_asuint(bc)) j->mis++;
         }
     return 0;
 }
@@ -38,8 +43,9 @@ static void* run_atan2(void* a) {
         default: y = (float)((int32_t)(r >> 32)) / 2147483648.0f * 4;
                  x = y * (1.0f + ((float)((int32_t)(xs(&s) >> 40)) / 8388608.0f) * 1e-3f); break;
         }
-        float a1 = atan2f(y, x), a2 = sdr_atan2f(y, x);
+        float a1 = atan2f(y, x), a2 = sdr_atan2f(y, x), a3 = sdr_atan2f_bf(y, x);
         if (sdr_asuint(a1) != sdr_asuint(a2) && !(isnan(a1) && isnan(a2))) j->mis++;
+        if (sdr_asuint(a1) != sdr_asuint(a3) && !(isnan(a1) && isnan(a3))) j->mis++;
     }
     return 0;
 }

@@ -59,24 +59,24 @@ __device__ __forceinline__ float2 frame_sample(const FrameSrc& s, long M, long f
     return make_float2(0.f, 0.f);
 }
 
-// -------- generic in-place Stockham pass over the 4096-point tile ----------------------
-// batch of 4096/M transforms of size M; radix R; stride Ns.  Each lane does 16/R butterflies.
-template <int R, bool INV>
-__device__ __forceinline__ void tile_pass(float2* lds, int M, int Ns, const float2* __restrict__ tw) {
+// -------- in-place Stockham pass over the 4096-point tile (all sizes compile-time) -----
+// batch of 4096/M transforms of size M; radix R; stride NS.  Each lane does 16/R butterflies.
+template <int R, int M, int NS, bool INV>
+__device__ __forceinline__ void tile_pass(float2* lds, const float2* __restrict__ tw) {
     constexpr int NBF = 16 / R;
+    constexpr int BPT = M / R;  // butterflies per transform
     const int t = threadIdx.x;
-    const int bpt = M / R;  // butterflies per transform
     float2 v[NBF][R];
 #pragma unroll
     for (int u = 0; u < NBF; ++u) {
         const int g = t * NBF + u;
-        const int f = g / bpt, j = g % bpt;
+        const int f = g / BPT, j = g % BPT;   // compile-time power-of-two divisors -> shifts
         const int base = f * M;
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[u][r] = lds[fpad(base + j + r * bpt)];
-        if (Ns > 1) {
-            const int k = j % Ns;
-            twiddle<R, INV>(v[u], tw, k * (kTile / (Ns * R)));
+        for (int r = 0; r < R; ++r) v[u][r] = lds[fpad(base + j + r * BPT)];
+        if (NS > 1) {
+            const int k = j % NS;
+            twiddle<R, INV>(v[u], tw, k * (kTile / (NS * R)));
         }
         Dft<R, INV>::run(v[u]);
     }
@@ -84,46 +84,45 @@ __device__ __forceinline__ void tile_pass(float2* lds, int M, int Ns, const floa
 #pragma unroll
     for (int u = 0; u < NBF; ++u) {
         const int g = t * NBF + u;
-        const int f = g / bpt, j = g % bpt;
-        const int k = j % Ns;
-        const int o = f * M + (j / Ns) * Ns * R + k;
+        const int f = g / BPT, j = g % BPT;
+        const int k = j % NS;
+        const int o = f * M + (j / NS) * NS * R + k;
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[fpad(o + r * Ns)] = v[u][r];
+        for (int r = 0; r < R; ++r) lds[fpad(o + r * NS)] = v[u][r];
     }
     __syncthreads();
 }
 
-template <bool INV>
-__device__ __forceinline__ void tile_fft(float2* lds, int M, const int* radix, int npass,
-                                         const float2* __restrict__ tw) {
-    int Ns = 1;
-    for (int p = 0; p < npass; ++p) {
-        switch (radix[p]) {
-        case 16: tile_pass<16, INV>(lds, M, Ns, tw); break;
-        case 8: tile_pass<8, INV>(lds, M, Ns, tw); break;
-        case 4: tile_pass<4, INV>(lds, M, Ns, tw); break;
-        default: tile_pass<2, INV>(lds, M, Ns, tw); break;
-        }
-        Ns *= radix[p];
+// radix plan: 16s first, then the remainder (M = 16^a * rem, rem in {1,2,4,8})
+template <int M, int NS, bool INV>
+__device__ __forceinline__ void tile_fft_rec(float2* lds, const float2* __restrict__ tw) {
+    if constexpr (NS < M) {
+        constexpr int LEFT = M / NS;
+        constexpr int R = LEFT >= 16 ? 16 : LEFT;
+        tile_pass<R, M, NS, INV>(lds, tw);
+        tile_fft_rec<M, NS * R, INV>(lds, tw);
     }
+}
+
+template <int M, bool INV>
+__device__ __forceinline__ void tile_fft(float2* lds, const float2* __restrict__ tw) {
+    tile_fft_rec<M, 1, INV>(lds, tw);
 }
 
 struct TileArgs {
     FrameSrc src;
     long nframes;      // frames this launch
     int M;
-    int radix[4];
-    int npass;
     const float2* tw;  // W_4096
     float norm;        // 1/sqrt(M) (f32, fft.rs:16)
     int store_mode;    // 0: collated (fft), 1: upper half of collated (rfft)
     float2* out;
 };
 
+template <int M>
 __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
     __shared__ float2 lds[kTileLds];
     const int t = threadIdx.x;
-    const int M = a.M;
     const int fpt = kTile / M;  // frames per tile
     const long f0 = (long)blockIdx.x * fpt;
     const int nf = (int)min((long)fpt, a.nframes - f0);
@@ -137,7 +136,7 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
         lds[fpad(p)] = x;
     }
     __syncthreads();
-    tile_fft<false>(lds, M, a.radix, a.npass, a.tw);
+    tile_fft<M, false>(lds, a.tw);
     // collated store: out[f][i] = X[(i + M/2) % M] * norm
     const int half = M / 2;
     if (a.store_mode == 0) {
@@ -171,8 +170,6 @@ struct FourArgs {
     FrameSrc src;
     long nframes;
     int M, M1, M2;
-    int radixA[4], npassA;  // M2 = prod radixA
-    int radixB[4], npassB;  // M1 = prod radixB
     const float2* tw;       // W_4096
     const float2* twM;      // W_M, M entries
     float norm;
@@ -180,10 +177,11 @@ struct FourArgs {
     float2* out;
 };
 
+template <int M2>
 __global__ __launch_bounds__(kFftBlock) void fft4_pass_a(FourArgs a) {
     __shared__ float2 lds[kTileLds];
     const int t = threadIdx.x;
-    const int C = kTile / a.M2;                  // columns per workgroup
+    constexpr int C = kTile / M2;                // columns per workgroup
     const int tiles_per_frame = a.M1 / C;
     const long f = blockIdx.x / tiles_per_frame;
     const int c0 = (int)(blockIdx.x % tiles_per_frame) * C;
@@ -194,29 +192,30 @@ __global__ __launch_bounds__(kFftBlock) void fft4_pass_a(FourArgs a) {
         const int p = t + kFftBlock * i;
         const int n2 = p / C, col = p % C;
         const float2 x = frame_sample(a.src, a.M, f, (long)(c0 + col) + (long)a.M1 * n2);
-        lds[fpad(col * a.M2 + n2)] = x;           // column-major: transform per column
+        lds[fpad(col * M2 + n2)] = x;             // column-major: transform per column
     }
     __syncthreads();
-    tile_fft<false>(lds, a.M2, a.radixA, a.npassA, a.tw);
+    tile_fft<M2, false>(lds, a.tw);
     // twiddle W_M^{n1 k2}, store S[n1][k2] (consecutive k2 contiguous)
     float2* S = a.scratch + f * (long)a.M;
 #pragma unroll 4
     for (int i = 0; i < 16; ++i) {
         const int p = t + kFftBlock * i;
-        const int col = p / a.M2, k2 = p % a.M2;
+        const int col = p / M2, k2 = p % M2;
         const int n1 = c0 + col;
-        float2 x = lds[fpad(col * a.M2 + k2)];
-        const long e = ((long)n1 * k2) % a.M;
+        float2 x = lds[fpad(col * M2 + k2)];
+        const int e = (n1 * k2) & (a.M - 1);      // M is a power of two
         x = cmul(x, a.twM[e]);
-        S[(long)n1 * a.M2 + k2] = x;
+        S[(long)n1 * M2 + k2] = x;
     }
 }
 
 // -------- four-step, pass B: M1-point FFTs over n1 for 4096/M1 consecutive k2 ----------
+template <int M1>
 __global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
     __shared__ float2 lds[kTileLds];
     const int t = threadIdx.x;
-    const int C = kTile / a.M1;                  // k2 columns per workgroup
+    constexpr int C = kTile / M1;                // k2 columns per workgroup
     const int tiles_per_frame = a.M2 / C;
     const long f = blockIdx.x / tiles_per_frame;
     const int c0 = (int)(blockIdx.x % tiles_per_frame) * C;
@@ -226,10 +225,10 @@ __global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
     for (int i = 0; i < 16; ++i) {
         const int p = t + kFftBlock * i;
         const int n1 = p / C, col = p % C;
-        lds[fpad(col * a.M1 + n1)] = S[(long)n1 * a.M2 + c0 + col];
+        lds[fpad(col * M1 + n1)] = S[(long)n1 * a.M2 + c0 + col];
     }
     __syncthreads();
-    tile_fft<false>(lds, a.M1, a.radixB, a.npassB, a.tw);
+    tile_fft<M1, false>(lds, a.tw);
     // X[k2 + M2 k1] -> collated out[(k + M/2) mod M] * norm ; lanes walk k2 (contiguous)
     float2* O = a.out + f * (long)a.M;
     const long half = a.M / 2;
@@ -240,20 +239,9 @@ __global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
         const long k = (long)(c0 + col) + (long)a.M2 * k1;
         long o = k + half;
         if (o >= a.M) o -= a.M;
-        const float2 x = lds[fpad(col * a.M1 + k1)];
+        const float2 x = lds[fpad(col * M1 + k1)];
         O[o] = make_float2(x.x * a.norm, x.y * a.norm);
     }
-}
-
-void radix_plan(int M, int* radix, int* npass) {
-    int n = 0;
-    while (M > 1) {
-        const int r = M >= 16 ? 16 : M;
-        // prefer balanced last stage (e.g. 64 = 16*4, 32 = 16*2)
-        radix[n++] = r;
-        M /= r;
-    }
-    *npass = n;
 }
 
 }  // namespace
@@ -341,14 +329,27 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         a.src = src;
         a.nframes = fr.nframes;
         a.M = p->M;
-        radix_plan(p->M, a.radix, &a.npass);
         a.tw = p->tw4096;
         a.norm = p->norm;
         a.store_mode = store_mode;
         a.out = out;
         const long fpt = kTile / p->M;
-        const long nblk = (fr.nframes + fpt - 1) / fpt;
-        hipLaunchKernelGGL(fft_tile_kernel, dim3((unsigned)nblk), dim3(kFftBlock), 0, s, a);
+        const dim3 g((unsigned)((fr.nframes + fpt - 1) / fpt)), b(kFftBlock);
+        switch (p->M) {
+        case 2: hipLaunchKernelGGL(fft_tile_kernel<2>, g, b, 0, s, a); break;
+        case 4: hipLaunchKernelGGL(fft_tile_kernel<4>, g, b, 0, s, a); break;
+        case 8: hipLaunchKernelGGL(fft_tile_kernel<8>, g, b, 0, s, a); break;
+        case 16: hipLaunchKernelGGL(fft_tile_kernel<16>, g, b, 0, s, a); break;
+        case 32: hipLaunchKernelGGL(fft_tile_kernel<32>, g, b, 0, s, a); break;
+        case 64: hipLaunchKernelGGL(fft_tile_kernel<64>, g, b, 0, s, a); break;
+        case 128: hipLaunchKernelGGL(fft_tile_kernel<128>, g, b, 0, s, a); break;
+        case 256: hipLaunchKernelGGL(fft_tile_kernel<256>, g, b, 0, s, a); break;
+        case 512: hipLaunchKernelGGL(fft_tile_kernel<512>, g, b, 0, s, a); break;
+        case 1024: hipLaunchKernelGGL(fft_tile_kernel<1024>, g, b, 0, s, a); break;
+        case 2048: hipLaunchKernelGGL(fft_tile_kernel<2048>, g, b, 0, s, a); break;
+        case 4096: hipLaunchKernelGGL(fft_tile_kernel<4096>, g, b, 0, s, a); break;
+        default: return SDRGPU_ERR_UNSUPPORTED;
+        }
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
     }
@@ -357,8 +358,6 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
     a.M = p->M;
     a.M1 = p->M1;
     a.M2 = p->M2;
-    radix_plan(p->M2, a.radixA, &a.npassA);
-    radix_plan(p->M1, a.radixB, &a.npassB);
     a.tw = p->tw4096;
     a.twM = p->twM;
     a.norm = p->norm;
@@ -372,9 +371,23 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         a.out = out + f0 * (long)p->M;
         const long ga = nf * (a.M1 / (kTile / a.M2));
         const long gb = nf * (a.M2 / (kTile / a.M1));
-        hipLaunchKernelGGL(fft4_pass_a, dim3((unsigned)ga), dim3(kFftBlock), 0, s, a);
+        const dim3 bA((unsigned)ga), bB((unsigned)gb), b(kFftBlock);
+        switch (a.M2) {
+        case 64: hipLaunchKernelGGL(fft4_pass_a<64>, bA, b, 0, s, a); break;
+        case 128: hipLaunchKernelGGL(fft4_pass_a<128>, bA, b, 0, s, a); break;
+        case 256: hipLaunchKernelGGL(fft4_pass_a<256>, bA, b, 0, s, a); break;
+        case 512: hipLaunchKernelGGL(fft4_pass_a<512>, bA, b, 0, s, a); break;
+        case 1024: hipLaunchKernelGGL(fft4_pass_a<1024>, bA, b, 0, s, a); break;
+        default: return SDRGPU_ERR_UNSUPPORTED;
+        }
         SDRGPU_LAUNCH_CHECK();
-        hipLaunchKernelGGL(fft4_pass_b, dim3((unsigned)gb), dim3(kFftBlock), 0, s, a);
+        switch (a.M1) {
+        case 128: hipLaunchKernelGGL(fft4_pass_b<128>, bB, b, 0, s, a); break;
+        case 256: hipLaunchKernelGGL(fft4_pass_b<256>, bB, b, 0, s, a); break;
+        case 512: hipLaunchKernelGGL(fft4_pass_b<512>, bB, b, 0, s, a); break;
+        case 1024: hipLaunchKernelGGL(fft4_pass_b<1024>, bB, b, 0, s, a); break;
+        default: return SDRGPU_ERR_UNSUPPORTED;
+        }
         SDRGPU_LAUNCH_CHECK();
     }
     return SDRGPU_OK;

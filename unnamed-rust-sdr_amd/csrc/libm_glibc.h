@@ -239,4 +239,99 @@ SDR_LIBM_FN float sdr_atan2f(float y, float x) {
     }
 }
 
+
+/* ---------------------------------------------------------------------------------------
+ * Branch-free forms for SIMD execution (a wave runs every taken path of a divergent
+ * branch).  Same per-lane arithmetic as the functions above -- only control flow differs:
+ *  - sincos: for |y| < 0.75 glibc skips reduce_fast, but there reduce_fast yields n = 0 and
+ *    x - 0*hpi == x exactly, so always reducing is bit-identical; one reduction feeds both
+ *    the sine and the cosine polynomial, and the quadrant picks which is sin and which cos.
+ *  - atanf: the five argument-reduction cases become selects of one numerator / one
+ *    denominator (each formed with the original operation order), then ONE division.
+ *  - atan2f: the sign quadrant switch becomes selects; true special cases (zero, inf, nan,
+ *    |y/x| beyond 2^+-60, x == 1) fall back to the reference function.
+ * Validated bit-exact against the host libm by tests/test_libm_restatement.py.
+ * ------------------------------------------------------------------------------------- */
+SDR_LIBM_FN void sdr_sincosf_bf(float y, float* sinp, float* cosp) {
+    int n;
+    const double xr = sdr_reduce_fast((double)y, &n);
+    const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+    const int neg = (n & 2) != 0;
+    const double xs = xr * s, x2 = xr * xr;
+    /* sine polynomial of xs (n even branch of sinf_poly) */
+    const double x3 = xs * x2;
+    const double s1 = SDR_MAD(x2, SDR_S3, SDR_S2);
+    const double x7 = x3 * x2;
+    const double ss = SDR_MAD(x3, SDR_S1, xs);
+    const float sp = (float)SDR_MAD(x7, s1, ss);
+    /* cosine polynomial (n odd branch), table[neg] */
+    const double c0 = neg ? -1.0 : 1.0;
+    const double kc1 = neg ? -SDR_C1 : SDR_C1, kc2 = neg ? -SDR_C2 : SDR_C2;
+    const double kc3 = neg ? -SDR_C3 : SDR_C3, kc4 = neg ? -SDR_C4 : SDR_C4;
+    const double x4 = x2 * x2;
+    const double c2 = SDR_MAD(x2, kc4, kc3);
+    const double c1 = SDR_MAD(x2, kc1, c0);
+    const double x6 = x4 * x2;
+    const double cc = SDR_MAD(x4, kc2, c1);
+    const float cp = (float)SDR_MAD(x6, c2, cc);
+    const int tiny = sdr_abstop12(y) < 0x398; /* |y| < 2^-12: sinf returns y, cosf 1 */
+    *sinp = tiny ? y : ((n & 1) ? cp : sp);
+    *cosp = tiny ? 1.0f : ((n & 1) ? sp : cp);
+}
+
+SDR_LIBM_FN float sdr_atanf_bf(float x) {
+    /* finite x (sdr_atan2f_bf routes NaN through the reference function) */
+    const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
+                atanhi2 = 9.8279368877e-01f, atanhi3 = 1.5707962513e+00f;
+    const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f,
+                atanlo2 = 3.4473217170e-08f, atanlo3 = 7.5497894159e-08f;
+    const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+                aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+                aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+                aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+    const float one = 1.0f;
+    const int32_t hx = (int32_t)sdr_asuint(x);
+    const int32_t ix = hx & 0x7fffffff;
+    const float ax = sdr_asfloat((uint32_t)ix);
+    /* id: -1 (|x| < 0.4375), 0, 1, 2, 3 */
+    const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float num0 = (float)2.0 * ax - one, den0 = (float)2.0 + ax;
+    const float num1 = ax - one, den1 = ax + one;
+    const float num2 = ax - (float)1.5, den2 = one + (float)1.5 * ax;
+    const float num = id == 0 ? num0 : id == 1 ? num1 : id == 2 ? num2 : -(float)1.0;
+    const float den = id == 0 ? den0 : id == 1 ? den1 : id == 2 ? den2 : ax;
+    const float q = num / den;
+    const float xr = id < 0 ? x : q;
+    const float z = xr * xr;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const float hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
+    const float lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+    const float rsmall = xr - xr * (s1 + s2);
+    const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
+    const float rbig = (hx < 0) ? -zz : zz;
+    /* |x| >= 2^25: +-(atanhi[3] + atanlo[3]); |x| < 2^-29: x itself (s_atanf.c) */
+    const float rhuge = (hx > 0) ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
+    return ix >= 0x4c000000 ? rhuge : ix < 0x31000000 ? x : id < 0 ? rsmall : rbig;
+}
+
+SDR_LIBM_FN float sdr_atan2f_bf(float y, float x) {
+    const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)sdr_asuint(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)sdr_asuint(y), iy = hy & 0x7fffffff;
+    const int32_t k = (iy - ix) >> 23;
+    /* common case: both finite and nonzero, x != 1, |k| <= 60 */
+    const int special = (ix >= 0x7f800000) | (iy >= 0x7f800000) | (ix == 0) | (iy == 0) |
+                        (hx == 0x3f800000) | (k > 60) | (k < -60);
+    if (special) return sdr_atan2f(y, x);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    const float qq = y / x;
+    const float z = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
+    const float t = z - pi_lo;
+    const float r2 = pi - t, r3 = t - pi;
+    const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
+    return m == 0 ? z : m == 1 ? r1 : m == 2 ? r2 : r3;
+}
+
 #endif /* SDR_LIBM_GLIBC_H */

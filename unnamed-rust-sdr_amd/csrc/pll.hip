@@ -84,13 +84,15 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
             lr = orr;
             li = oi;
         }
-        const float phasedif = sdr_atan2f(li, lr) * p.gain;       // :72 arg() * gain
+        const float phasedif = sdr_atan2f_bf(li, lr) * p.gain;    // :72 arg() * gain
         float nph = s.nphase + (p.reference + phasedif);           // :73
         nph = nph - truncf(nph);                                   // :74 fract()
         s.nphase = nph;
         const float phase = kTwoPi * nph;                          // :75
-        s.vr = 1.0f * sdr_cosf(phase);                             // :76 from_polar
-        s.vi = 1.0f * sdr_sinf(phase);
+        float sn, cs;
+        sdr_sincosf_bf(phase, &sn, &cs);                           // glibc sinf/cosf, branch-free
+        s.vr = 1.0f * cs;                                          // :76 from_polar
+        s.vi = 1.0f * sn;
         const float lockv = p.lock_ident ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
         const float o = p.out_ident ? phasedif * p.rate
                                     : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
