@@ -16,6 +16,8 @@
 // does R*R MACs per R LDS reads.
 // Roofline: 2*K (real taps) / 8*K (complex taps) flops per kept output; for K=255, D=4 on
 // c64 it is FP32-VALU bound, see DESIGN.md.
+#include <cstdlib>
+
 #include "fir_kernels.hpp"
 
 namespace sdrgpu {
@@ -182,6 +184,11 @@ int dispatch_direct(const FirParams& p, hipStream_t s) {
 }  // namespace
 
 int fir_direct_launch(const FirParams& p, hipStream_t s) {
+    static const bool v1_only = [] {
+        const char* e = getenv("SDRGPU_DIRECT_V1");
+        return e && atoi(e) != 0;
+    }();
+    if (!v1_only && !p.force_naive && fir_direct2_supported(p)) return fir_direct2_launch(p, s);
     if (p.sample_kind == SDRGPU_F32 && p.tap_kind == SDRGPU_F32)
         return dispatch_direct<float, float>(p, s);
     if (p.sample_kind == SDRGPU_C64 && p.tap_kind == SDRGPU_F32)

@@ -6,8 +6,8 @@
 namespace sdrgpu {
 
 // Taps are kept on the device in polyphase-major order: taps_pm[p*tpp + i] = h[p + i*D]
-// (zero beyond K), tpp = ceil(ceil(K/D) / 8) * 8.
-constexpr int kTapPad = 8;
+// (zero beyond K), tpp = ceil(ceil(K/D) / 16) * 16.
+constexpr int kTapPad = 16;
 
 inline int taps_per_phase(int K, int D) {
     int t = (K + D - 1) / D;
@@ -33,6 +33,11 @@ struct FirParams {
 };
 
 int fir_direct_launch(const FirParams& p, hipStream_t s);
+
+// Wave-private persistent direct form (fir_direct2.hip): c64 samples, f32 taps,
+// D in {1,2,4,8}, D*tpp <= 1024.  Returns SDRGPU_ERR_UNSUPPORTED otherwise.
+bool fir_direct2_supported(const FirParams& p);
+int fir_direct2_launch(const FirParams& p, hipStream_t s);
 
 // Overlap-save (polyphase, LDS-resident FFT) path; returns SDRGPU_ERR_UNSUPPORTED for
 // shapes it does not cover (caller falls back to direct).
