@@ -774,6 +774,203 @@ struct OsState {
     float2* d_tw = nullptr;
 };
 
+// ---------------------------------------------------------------------------------
+// v5 (D = 4): three workgroup barriers per window, wave-local inverse FFTs.
+//
+// Forward, per window (4 branches x 1024 points, 256 lanes x 16 points):
+//   branch element j = 64 n1 + n2, bin k = k1 + 16 k2, k2 = j1 + 16 j2, n2 = 4 m1 + m2
+//   P1  lane t (n2 = t/4, branch 3 - t%4): 16-pt DFT over n1 of its 16 coalesced samples,
+//       x W1024^(n2 k1) (per-lane constant twiddles), -> LDS A[b][k1][n2]         | barrier
+//   P2  wave b, lane (k1, m2): 16-pt DFT over m1 of A[b][k1][4 m1 + m2], x W64^(m2 j1)
+//       -> LDS B[b][m2][k1 + 16 j1] (wave-local: this wave's branch only)        | barrier
+//   P3  lane kappa = k1 + 16 j1: 4-pt DFT over m2 per branch -> X_b[kappa + 256 j2],
+//       Y = sum_b H_b X_b with H held in registers -> spectrum slot w (LDS)       | barrier
+// Inverse, every 4 windows, wave v on slot v (64 lanes x 16 points, no barriers):
+//   k = 64 k1 + k2, n = n1 + 16 n2, k2 = 16 c + a, n2 = d + 4 e
+//   I1  lane k2: 16-pt IDFT over k1, x W1024^-(n1 k2)            -> E1[n1][k2]
+//   I2  lane (a, n1 = l/16 + 4 i): 4-pt IDFT over c, x W64^-(d a)  -> E2[n1][d][a]
+//   I3  lane n1 + 16 d: 16-pt IDFT over a -> y[lane + 64 e]: coalesced stores
+// The next window's samples are loaded into the registers P1 has just consumed, so they
+// stream in during P2, P3 and the inverse.  LDS: workspace 4 x 1092 + 4 spectrum slots x
+// 1280 float2 = 75 KiB (2 workgroups per CU).
+constexpr int kOs5Slot = 1280;
+constexpr int kOs5Br = 1092;   // branch stride (== 4 mod 16)
+
+__global__ __launch_bounds__(kOsBlock, 2) void fir_os5_kernel(OsParams p, long nblk) {
+    constexpr int D = 4, L = 1024;
+    __shared__ float2 ws[4 * kOs5Br];
+    __shared__ float2 slots[4 * kOs5Slot];
+    __shared__ float2 t64[64];  // W64^(m2 j1) at [16 m2 + j1]
+
+    const long ch = blockIdx.y;
+    const float2* __restrict__ in = p.in + ch * p.ld_in;
+    const float2* __restrict__ hist = p.hist + ch * (long)(p.K - 1);
+    float2* __restrict__ out = p.out + ch * p.ld_out;
+    const float2* __restrict__ tw = p.tw;  // W4096^m
+    const int K = p.K;
+    const int skip = L - p.M;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+
+    // ---- per-lane constants ----
+    float2 w1[16], wi2[4];
+    const float2 wi1b = conjf2(tw[(4 * lane) & 4095]);  // W1024^-(k2), k2 = lane
+    if (t < 64) t64[t] = tw[(64 * (t >> 4) * (t & 15)) & 4095];
+    {
+        const int n2 = t >> 2;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            w1[r] = tw[(4 * n2 * r) & 4095];                 // W1024^(n2 r)
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) wi2[d] = conjf2(tw[(64 * d * (lane & 15)) & 4095]);  // W64^-(d a)
+    }
+    float2 H[4][4];  // H[b][j2] = H_b[kappa + 256 j2], kappa = t
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int j2 = 0; j2 < 4; ++j2) H[b][j2] = p.H[b * L + t + 256 * j2];
+
+    const long hop = (long)p.M * D;
+    const long nquad = (nblk + 3) / 4;
+    float2 v[16];
+    long quad = blockIdx.x;
+    auto base_of = [&](long q) { return p.i0 + (q * p.M + p.M - L) * (long)D - (D - 1); };
+    if (quad < nquad) os2_load<D>(v, in, hist, p.n_in, K, base_of(4 * quad) + t);
+
+#pragma unroll 1
+    for (; quad < nquad; quad += gridDim.x) {
+#pragma unroll 1
+        for (int w = 0; w < 4; ++w) {
+            const long q = 4 * quad + w;
+            // ---- P1 ----
+            Dft<16, false>::run(v);
+            {
+                const int n2 = t >> 2, b = 3 - (t & 3);
+                float2* dst = ws + b * kOs5Br + n2;
+                dst[0] = v[0];
+#pragma unroll
+                for (int k1 = 1; k1 < 16; ++k1) dst[68 * k1] = cmul(v[k1], w1[k1]);
+            }
+            // ---- next window's samples fly during P2 / P3 / inverse ----
+            {
+                const long qn = (w < 3) ? q + 1 : 4 * (quad + gridDim.x);
+                if (qn < 4 * nquad) os2_load<D>(v, in, hist, p.n_in, K, base_of(qn) + t);
+            }
+            __syncthreads();
+            // ---- P2 (wave-local: wave = branch) ----
+            {
+                const int k1 = lane >> 2, m2 = lane & 3;
+                float2* rb = ws + wave * kOs5Br + 68 * k1 + m2;
+                float2 u[16];
+#pragma unroll
+                for (int m1 = 0; m1 < 16; ++m1) u[m1] = rb[4 * m1];
+                Dft<16, false>::run(u);
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                float2* wb = ws + wave * kOs5Br + 260 * m2 + k1;
+                const float2* tr = t64 + 16 * m2;
+                wb[0] = u[0];
+#pragma unroll
+                for (int j1 = 1; j1 < 16; ++j1) wb[16 * j1] = cmul(u[j1], tr[j1]);
+            }
+            __syncthreads();
+            // ---- P3: 4-pt DFTs, multiply by H, sum over branches ----
+            {
+                float2 y[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const float2* rb = ws + b * kOs5Br + t;
+                    float2 a0 = rb[0], a1 = rb[260], a2 = rb[520], a3 = rb[780];
+                    dft4<false>(a0, a1, a2, a3);
+                    if (b == 0) {
+                        y[0] = cmul(a0, H[0][0]);
+                        y[1] = cmul(a1, H[0][1]);
+                        y[2] = cmul(a2, H[0][2]);
+                        y[3] = cmul(a3, H[0][3]);
+                    } else {
+                        const float2 x4[4] = {a0, a1, a2, a3};
+#pragma unroll
+                        for (int j2 = 0; j2 < 4; ++j2) {
+                            y[j2].x = fmaf(x4[j2].x, H[b][j2].x, fmaf(-x4[j2].y, H[b][j2].y, y[j2].x));
+                            y[j2].y = fmaf(x4[j2].x, H[b][j2].y, fmaf(x4[j2].y, H[b][j2].x, y[j2].y));
+                        }
+                    }
+                }
+                float2* sl = slots + w * kOs5Slot + t;
+#pragma unroll
+                for (int j2 = 0; j2 < 4; ++j2) sl[256 * j2] = y[j2];
+            }
+            __syncthreads();
+        }
+
+        // ---- inverse: wave v transforms slot v (window 4 quad + v) ----
+        {
+            const long q = 4 * quad + wave;
+            float2* sl = slots + wave * kOs5Slot;
+            float2 u[16];
+            // I1: lane = k2
+#pragma unroll
+            for (int k1 = 0; k1 < 16; ++k1) u[k1] = sl[64 * k1 + lane];
+            Dft<16, true>::run(u);
+            {
+                // x W1024^-(n1 k2): powers of the lane's base (once per 4 windows)
+                float2 wb = wi1b;
+                asm volatile("" : "+v"(wb.x), "+v"(wb.y));
+                twiddle_tree<16>(u, wb);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int n1 = 0; n1 < 16; ++n1) sl[80 * n1 + lane] = u[n1];
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // I2: lane (a, n1 = lane/16 + 4 i)
+            const int a = lane & 15, nb = lane >> 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) u[4 * i + c] = sl[80 * (nb + 4 * i) + 16 * c + a];
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dft4<true>(u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3]);
+                float2* wr = sl + 65 * (nb + 4 * i) + a;
+                wr[0] = u[4 * i];
+#pragma unroll
+                for (int d = 1; d < 4; ++d) wr[16 * d] = cmul(u[4 * i + d], wi2[d]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // I3: lane = n1 + 16 d
+            {
+                const int n1 = lane & 15, d = lane >> 4;
+#pragma unroll
+                for (int aa = 0; aa < 16; ++aa) u[aa] = sl[65 * n1 + 16 * d + aa];
+            }
+            Dft<16, true>::run(u);
+            if (q < nblk) {
+                const long m0 = q * p.M - skip + lane;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int n = lane + 64 * e;
+                    if (n >= skip && m0 + 64 * e < p.n_out) out[m0 + 64 * e] = u[e];
+                }
+            }
+        }
+        // slots are rewritten by the next quad's P3 only after two more barriers
+    }
+
+    if (blockIdx.x == gridDim.x - 1) {  // stream history carry (see fir_direct.hip)
+        float2* hn = p.hist_next + ch * (long)(K - 1);
+        for (int jj = t; jj < K - 1; jj += kOsBlock) {
+            const long g = p.n_in - (long)(K - 1) + jj;
+            hn[jj] = g >= 0 ? in[g] : hist[g + (K - 1)];
+        }
+    }
+}
+
 int os_geometry(int K, int D, int* L, int* M) {
     if (!(D == 1 || D == 2 || D == 4 || D == 8)) return 0;
     const int l = kOsPoints / D;
@@ -893,6 +1090,11 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
         else if (variant == 5) hipLaunchKernelGGL((fir_os4_kernel<8>), pgrid, dim3(kOs4Block), 0, s, p, nblk);
         else if (variant == 7) hipLaunchKernelGGL((fir_os3_kernel<4, 1, 4, 1>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else if (variant == 8) hipLaunchKernelGGL((fir_os3_kernel<4, 1, 4, 2>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 9) {
+            const long nquad = (nblk + 3) / 4;
+            dim3 g5((unsigned)std::max(1L, std::min(nquad, (256L * 2 + fp.nch - 1) / fp.nch)), (unsigned)fp.nch);
+            hipLaunchKernelGGL(fir_os5_kernel, g5, dim3(kOsBlock), 0, s, p, nblk);
+        }
         else if (variant == 6) hipLaunchKernelGGL((fir_os4_kernel<6>), pgrid, dim3(kOs4Block), 0, s, p, nblk);
         else hipLaunchKernelGGL(fir_os_kernel<4>, grid, dim3(kOsBlock), 0, s, p);
         break;
