@@ -7,66 +7,89 @@
 namespace sdrgpu {
 namespace fftd {
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Native 2-wide vector view of a complex value: one VGPR pair, so complex adds are single
+// v_pk_add_f32 and the +-i rotations below fold into that instruction's op_sel / neg bits
+// (the compiler does not form those from float2 struct code and emits swaps instead).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v vv(float2 a) { return __builtin_bit_cast(f2v, a); }
+__device__ __forceinline__ float2 ff(f2v a) { return __builtin_bit_cast(float2, a); }
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return ff(vv(a) + vv(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return ff(vv(a) - vv(b)); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+
+// a + (-i) b = (a.x + b.y, a.y - b.x): one v_pk_add_f32 (src1 halves swapped, hi negated)
+__device__ __forceinline__ f2v add_mi(f2v a, f2v b) {
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// a - (-i) b = a + i b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ f2v sub_mi(f2v a, f2v b) {
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
-    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+    const f2v z = {0.f, 0.f};
+    return ff(INV ? sub_mi(z, vv(a)) : add_mi(z, vv(a)));
 }
 
-// exp(-+2 pi i m / 16) for m = 0..15 (sign applied by caller via INV)
-__device__ __forceinline__ float2 w16(int m) {
-    constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f;
-    constexpr float c2 = 0.70710678118654752f;
-    switch (m & 15) {
-    case 0: return make_float2(1.f, 0.f);
-    case 1: return make_float2(c1, -s1);
-    case 2: return make_float2(c2, -c2);
-    case 3: return make_float2(s1, -c1);
-    case 4: return make_float2(0.f, -1.f);
-    case 5: return make_float2(-s1, -c1);
-    case 6: return make_float2(-c2, -c2);
-    case 7: return make_float2(-c1, -s1);
-    case 8: return make_float2(-1.f, 0.f);
-    case 9: return make_float2(-c1, s1);
-    case 10: return make_float2(-c2, c2);
-    case 11: return make_float2(-s1, c1);
-    case 12: return make_float2(0.f, 1.f);
-    case 13: return make_float2(s1, c1);
-    case 14: return make_float2(c2, c2);
-    default: return make_float2(c1, s1);
-    }
-}
-
+// a * W16^m (forward sign) or a * conj(W16^m) (inverse); m = 0..15
 template <bool INV>
 __device__ __forceinline__ float2 twm(float2 a, int m16) {
-    // a * W16^m (forward sign) or a * conj(W16^m) (inverse)
-    float2 w = w16(m16);
+    constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f;
+    constexpr float c2 = 0.70710678118654752f;
+    const f2v x = vv(a);
+    const f2v z = {0.f, 0.f};
+    switch (m16 & 15) {
+    case 0: return a;
+    case 2: return ff((INV ? sub_mi(x, x) : add_mi(x, x)) * c2);      // (1 -+ i)/sqrt2
+    case 4: return ff(INV ? sub_mi(z, x) : add_mi(z, x));              // -+i
+    case 6: return ff((INV ? add_mi(x, x) : sub_mi(x, x)) * (-c2));   // (-1 -+ i)/sqrt2
+    case 8: return ff(-x);
+    case 10: return ff((INV ? sub_mi(x, x) : add_mi(x, x)) * (-c2));  // (-1 +- i)/sqrt2
+    case 12: return ff(INV ? add_mi(z, x) : sub_mi(z, x));             // +-i
+    case 14: return ff((INV ? add_mi(x, x) : sub_mi(x, x)) * c2);     // (1 +- i)/sqrt2
+    default: break;
+    }
+    // generic: the W16 table value (conjugated for the inverse)
+    float2 w;
+    switch (m16 & 15) {
+    case 1: w = make_float2(c1, -s1); break;
+    case 3: w = make_float2(s1, -c1); break;
+    case 5: w = make_float2(-s1, -c1); break;
+    case 7: w = make_float2(-c1, -s1); break;
+    case 9: w = make_float2(-c1, s1); break;
+    case 11: w = make_float2(-s1, c1); break;
+    case 13: w = make_float2(s1, c1); break;
+    default: w = make_float2(c1, s1); break;
+    }
     if (INV) w.y = -w.y;
     return cmul(a, w);
 }
 
 template <bool INV>
 __device__ __forceinline__ void dft2(float2& a, float2& b) {
-    float2 t = a;
-    a = cadd(t, b);
-    b = csub(t, b);
+    const f2v t = vv(a), u = vv(b);
+    a = ff(t + u);
+    b = ff(t - u);
 }
 
-// in-place 4-point DFT, natural-order output
+// in-place 4-point DFT, natural-order output: 8 v_pk_add_f32
 template <bool INV>
 __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
-    float2 s02 = cadd(a0, a2), d02 = csub(a0, a2);
-    float2 s13 = cadd(a1, a3), d13 = mul_mi<INV>(csub(a1, a3));
-    a0 = cadd(s02, s13);
-    a2 = csub(s02, s13);
-    a1 = cadd(d02, d13);
-    a3 = csub(d02, d13);
+    const f2v x0 = vv(a0), x1 = vv(a1), x2 = vv(a2), x3 = vv(a3);
+    const f2v s02 = x0 + x2, d02 = x0 - x2, s13 = x1 + x3, d13 = x1 - x3;
+    a0 = ff(s02 + s13);
+    a2 = ff(s02 - s13);
+    a1 = ff(INV ? sub_mi(d02, d13) : add_mi(d02, d13));
+    a3 = ff(INV ? add_mi(d02, d13) : sub_mi(d02, d13));
 }
 
 // generic R = R1*R2 split: n = R2*n1 + n2 ; k = k1 + R1*k2
