@@ -234,7 +234,10 @@ __device__ __forceinline__ void os2_load(float2 (&v)[16], const float2* __restri
     }
 }
 
-template <int D, bool PF, int W>
+// HR: the lane's D*R3 branch-spectrum values H_b[t + 256 r] are loaded once into registers
+// instead of from L2 every window (the per-window H loads double the vector-memory
+// instructions of the stream)
+template <int D, bool PF, int W, bool HR = false>
 __global__ __launch_bounds__(kOsBlock, W) void fir_os2_kernel(OsParams p, long nblk) {
     constexpr int L = kOsPoints / D;
     constexpr int R3 = L / 256;
@@ -270,6 +273,13 @@ __global__ __launch_bounds__(kOsBlock, W) void fir_os2_kernel(OsParams p, long n
         wib[s] = conjf2(tw[k * (kOsPoints / (4 * Ns))]);
     }
 
+    float2 hreg[HR ? D * R3 : 1];
+    if (HR) {
+#pragma unroll
+        for (int b = 0; b < D; ++b)
+#pragma unroll
+            for (int r = 0; r < R3; ++r) hreg[HR ? b * R3 + r : 0] = p.H[b * L + 256 * r + t0];
+    }
     float2 v[16];
     long q = blockIdx.x;
     const long hop = (long)p.M * D;
@@ -332,7 +342,7 @@ __global__ __launch_bounds__(kOsBlock, W) void fir_os2_kernel(OsParams p, long n
                 Dft<R3, false>::run(w);
 #pragma unroll
                 for (int r = 0; r < R3; ++r) {
-                    const float2 h = H[b * L + 256 * r];
+                    const float2 h = HR ? hreg[HR ? b * R3 + r : 0] : H[b * L + 256 * r];
                     z[r].x = fmaf(w[r].x, h.x, fmaf(-w[r].y, h.y, z[r].x));
                     z[r].y = fmaf(w[r].x, h.y, fmaf(w[r].y, h.x, z[r].y));
                 }
@@ -1068,13 +1078,18 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
     p.ld_out = fp.ld_out;
     const long nblk = fp.n_out > 0 ? ceil_div(fp.n_out, st->M) : 1;
     dim3 grid((unsigned)nblk, (unsigned)fp.nch);
-    // v2 variants (debug knob SDRGPU_OS_VARIANT): 0 = persistent + prefetch, 3 waves/SIMD
-    // (default); 1 = persistent, no prefetch, 4 waves/SIMD; 2 = v1 (one block per WG).
+    // Kernel variants (debug/A-B knob SDRGPU_OS_VARIANT; all parity-tested), D = 4 | 8:
+    //   11 (default) persistent v2, branch spectra in registers, 4 WG/CU
+    //    1 persistent v2, spectra re-read from L2 every window      0 / 10 + next-window prefetch
+    //    2 v1 (one window per workgroup)   3 / 4 two / one windows per iteration (v3)
+    //    5 / 6 512-lane radix-8 (v4)       9 three-barrier, wave-local inverse (v5)
+    //    7 / 8 ablations: memory only / FFT only (results invalid)
+    //   12 = 11 at 3 WG/CU
     static const char* var_env = getenv("SDRGPU_OS_VARIANT");
     static const char* force_v1 = getenv("SDRGPU_OS_V1");
-    int variant = var_env ? atoi(var_env) : 1;
+    int variant = var_env ? atoi(var_env) : 11;
     if (force_v1 && force_v1[0] == '1') variant = 2;
-    const int wgs_per_cu = variant == 1 ? 4 : variant == 3 ? 2 : variant == 4 ? 4 : variant == 5 ? 4 : variant == 6 ? 3 : variant >= 7 ? 4 : 3;
+    const int wgs_per_cu = variant == 1 ? 4 : variant == 3 ? 2 : variant == 4 ? 4 : variant == 5 ? 4 : variant == 6 ? 3 : variant == 12 ? 3 : variant >= 7 ? 4 : 3;  // 11/12: H in registers at 4/3 WG per CU
     const long per_ch = std::max(1L, std::min(nblk, (256L * wgs_per_cu + fp.nch - 1) / fp.nch));
     const long per_ch2 = std::max(1L, std::min((nblk + 1) / 2, (256L * wgs_per_cu + fp.nch - 1) / fp.nch));
     dim3 pgrid2((unsigned)per_ch2, (unsigned)fp.nch);
@@ -1090,6 +1105,9 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
         else if (variant == 5) hipLaunchKernelGGL((fir_os4_kernel<8>), pgrid, dim3(kOs4Block), 0, s, p, nblk);
         else if (variant == 7) hipLaunchKernelGGL((fir_os3_kernel<4, 1, 4, 1>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else if (variant == 8) hipLaunchKernelGGL((fir_os3_kernel<4, 1, 4, 2>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 10) hipLaunchKernelGGL((fir_os2_kernel<4, true, 4>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 11) hipLaunchKernelGGL((fir_os2_kernel<4, false, 4, true>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
+        else if (variant == 12) hipLaunchKernelGGL((fir_os2_kernel<4, false, 3, true>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else if (variant == 9) {
             const long nquad = (nblk + 3) / 4;
             dim3 g5((unsigned)std::max(1L, std::min(nquad, (256L * 2 + fp.nch - 1) / fp.nch)), (unsigned)fp.nch);
@@ -1101,7 +1119,8 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
     case 8:
         if (variant == 0) hipLaunchKernelGGL((fir_os2_kernel<8, true, 3>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         else if (variant == 1) hipLaunchKernelGGL((fir_os2_kernel<8, false, 4>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
-        else hipLaunchKernelGGL(fir_os_kernel<8>, grid, dim3(kOsBlock), 0, s, p);
+        else if (variant == 2) hipLaunchKernelGGL(fir_os_kernel<8>, grid, dim3(kOsBlock), 0, s, p);
+        else hipLaunchKernelGGL((fir_os2_kernel<8, false, 4, true>), pgrid, dim3(kOsBlock), 0, s, p, nblk);
         break;
     default: return SDRGPU_ERR_UNSUPPORTED;
     }
