@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=28, help="input samples per GPU per step")
-    ap.add_argument("--algo", default="auto", choices=["auto", "direct", "os"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "direct", "os", "mx"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_fir_c2.json"))
@@ -132,7 +132,8 @@ def main():
     taps = ss.firwin(255, 0.2).astype(np.float32)
     n = 1 << args.log2n
     D = 4
-    algo = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE}[args.algo]
+    algo = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE,
+            "mx": _lib.FIR_MATRIX}[args.algo]
     fir = sdrgpu.filter.Fir(taps, decim=D, sample_kind=_lib.C64, device=local,
                             algorithm=algo).design(2.4e6)
     stream = fir.stream()

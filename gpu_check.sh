@@ -1,0 +1,13 @@
+#!/bin/bash
+# Sanity pass: GPU tests + smoke + default bench.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/check
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 2; }
+cat $O/smoke.log
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 3; }
+tail -1 $O/bench.log

@@ -59,6 +59,8 @@ enum sdrgpu_fir_algo {
     SDRGPU_FIR_AUTO = 0,          /* pick per shape */
     SDRGPU_FIR_DIRECT = 1,        /* LDS-tiled direct form, register-blocked outputs */
     SDRGPU_FIR_OVERLAP_SAVE = 2,  /* polyphase overlap-save, LDS-resident FFT tiles */
+    SDRGPU_FIR_MATRIX = 3,        /* direct form on bf16 MFMA with an exact 3-way f32 split
+                                     (c64 samples, f32 taps, decim 2/4/8, 16-B aligned input) */
 };
 
 const char* sdrgpu_strerror(int code);   /* resample::Error Display, src/resample.rs:209-269 */

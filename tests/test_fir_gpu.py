@@ -27,17 +27,18 @@ def make_case(rng, sk, tk, K, n):
     return taps, x
 
 
-ALGOS = ["direct", "os", "auto"]
+ALGOS = ["direct", "os", "mx", "auto"]
 
 
 def fir(sdr, taps, sk, D, algo="auto"):
     from sdrgpu import _lib
-    a = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE}[algo]
+    a = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE,
+         "mx": _lib.FIR_MATRIX}[algo]
     try:
         return sdr.filter.Fir(taps, decim=D, sample_kind=sk, algorithm=a).design(2.4e6)
     except _lib.SdrGpuError as e:
-        if e.code == _lib.ERR_UNSUPPORTED and algo == "os":
-            pytest.skip("overlap-save does not cover this shape")
+        if e.code == _lib.ERR_UNSUPPORTED and algo in ("os", "mx"):
+            pytest.skip(f"{algo} does not cover this shape")
         raise
 
 
@@ -59,6 +60,11 @@ CASES = [
     (1, 0, 255, 8, 30000),     # overlap-save D=8
     (1, 1, 1000, 1, 20000),    # overlap-save D=1, long complex filter
     (1, 0, 2, 4, 5000),        # shortest filter with history
+    (1, 0, 255, 4, 333333),    # MFMA path: many segments, ragged last segment
+    (1, 0, 61, 4, 7777),       # MFMA path: short filter (4 chunks)
+    (1, 0, 100, 2, 20001),     # MFMA D=2, odd length
+    (1, 0, 200, 8, 65537),     # MFMA D=8
+    (1, 0, 1, 2, 1000),        # MFMA single tap
 ]
 
 
@@ -72,6 +78,43 @@ def test_fir_parity(sdr, oracle, case, algo):
     y = fir(sdr, taps, sk, D, algo).process(x)
     assert y.shape == ref.shape
     assert_parity(y, ref, what=str(case))
+
+
+@pytest.mark.parametrize("scale", [1e-30, 1e-6, 1e6, 1e30])
+def test_fir_mx_dynamic_range(sdr, oracle, scale):
+    """The exact 3-way bf16 split keeps f32's exponent range: tiny and huge inputs."""
+    rng = np.random.default_rng(17)
+    taps, x = make_case(rng, 1, 0, 255, 20000)
+    x = (x * np.float32(scale)).astype(np.complex64)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(x)
+    y = fir(sdr, taps, 1, 4, "mx").process(x)
+    assert_parity(y, ref, what=f"scale {scale}")
+
+
+@pytest.mark.parametrize("phase", [0, 1, 2, 3])
+def test_fir_mx_decimation_phase(sdr, oracle, phase):
+    """Every decimation phase (window alignment delta = 0/1) after a ragged first block."""
+    rng = np.random.default_rng(23 + phase)
+    taps, x = make_case(rng, 1, 0, 255, 30000)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(x)
+    f = fir(sdr, taps, 1, 4, "mx")
+    y = np.concatenate([f.process(x[:phase + 1]), f.process(x[phase + 1:])])
+    assert_parity(y, ref, what=f"phase {phase}")
+
+
+def test_fir_mx_unaligned_device_pointer(sdr, oracle):
+    """An input pointer that is not 16-byte aligned falls back to another path."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(29)
+    taps, x = make_case(rng, 1, 0, 255, 40001)
+    f = fir(sdr, taps, 1, 4, "mx")
+    dx = DeviceBuffer.from_numpy(x)
+    n = x.size - 1
+    n_out = f.output_len(n)
+    dy = DeviceBuffer.empty(n_out, np.complex64)
+    assert f.process_dev(dx.ptr + 8, n, dy.ptr, n_out) == n_out
+    f.sync()
+    assert_parity(dy.download(), oracle.Fir(taps, 4, sample_kind=1).process(x[1:]))
 
 
 @pytest.mark.parametrize("name", ["fir_c1.npz", "fir_c2.npz", "fir_cc.npz"])
@@ -155,16 +198,20 @@ def test_fir_reset_and_clone(sdr, oracle):
     assert_parity(np.concatenate([a, b1]), ref)
 
 
-def test_firbank_parity(sdr, oracle):
+@pytest.mark.parametrize("algo", ["auto", "mx", "os", "direct"])
+def test_firbank_parity(sdr, oracle, algo):
+    from sdrgpu import _lib
     rng = np.random.default_rng(5)
     nch, n, K, D = 37, 5000, 255, 4
     taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
     x = cplx(rng, nch * n).reshape(nch, n)
     ref = oracle.fir_batch(taps, x, D, nthreads=8)
-    bank = sdr.filter.FirBank(taps, nch, sample_kind=1, decim=D)
-    y1 = bank.process(x[:, :1234])
-    y2 = bank.process(x[:, 1234:])
-    y = np.concatenate([y1, y2], axis=1)
+    a = {"auto": _lib.FIR_AUTO, "direct": _lib.FIR_DIRECT, "os": _lib.FIR_OVERLAP_SAVE,
+         "mx": _lib.FIR_MATRIX}[algo]
+    bank = sdr.filter.FirBank(taps, nch, sample_kind=1, decim=D, algorithm=a)
+    # 1111 is odd: the MFMA path needs even channel strides and hands that block on
+    y = np.concatenate([bank.process(x[:, :1234]), bank.process(x[:, 1234:2345]),
+                        bank.process(x[:, 2345:])], axis=1)
     assert y.shape == ref.shape
     for c in range(nch):
         assert_parity(y[c], ref[c], what=f"ch{c}")
@@ -237,7 +284,7 @@ def test_fir_full_size_c2_properties(sdr, oracle):
         assert np.array_equal(y2, 2 * y1)
 
 
-@pytest.mark.parametrize("algo", ["direct", "auto"])
+@pytest.mark.parametrize("algo", ["direct", "mx", "auto"])
 def test_time_shard_halo_equivalence(sdr, oracle, algo):
     """Multi-GPU time sharding (bench.py): a shard primed with the 256 preceding samples
     produces exactly the continuation of the unsharded stream."""

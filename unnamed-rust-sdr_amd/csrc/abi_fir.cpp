@@ -17,6 +17,10 @@ int fir_os_launch(const FirParams& p, void* os_state, hipStream_t s);
 void* fir_os_prepare(int device, int sample_kind, int tap_kind, const void* taps, int K,
                      int D, hipStream_t s, int* status);
 void fir_os_release(void* os_state);
+int fir_mx_supported(int sample_kind, int tap_kind, int K, int D);
+void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status);
+int fir_mx_launch(const FirParams& p, void* state, hipStream_t s);
+void fir_mx_release(void* state);
 }  // namespace sdrgpu
 
 struct FirCore {
@@ -35,6 +39,8 @@ struct FirCore {
     DevBuf stage_in, stage_out;
     void* os_state = nullptr;              // overlap-save plan (lazily built)
     int os_status = SDRGPU_OK;
+    void* mx_state = nullptr;              // split-bf16 MFMA direct-form plan (lazily built)
+    int mx_status = SDRGPU_OK;
 
     size_t sbytes() const { return kind_bytes(sk); }
     size_t hist_bytes() const { return nch * (size_t)(K - 1) * sbytes(); }
@@ -59,6 +65,8 @@ struct FirCore {
         stage_out.release();
         if (os_state) fir_os_release(os_state);
         os_state = nullptr;
+        if (mx_state) fir_mx_release(mx_state);
+        mx_state = nullptr;
         stream.destroy();
     }
 
@@ -111,8 +119,13 @@ struct FirCore {
         return reset_state();
     }
 
+    bool want_mx() const {
+        if (algo != SDRGPU_FIR_AUTO && algo != SDRGPU_FIR_MATRIX) return false;
+        return fir_mx_supported(sk, tk, K, D) != 0;
+    }
+
     bool want_os() const {
-        if (algo == SDRGPU_FIR_DIRECT) return false;
+        if (algo == SDRGPU_FIR_DIRECT || algo == SDRGPU_FIR_MATRIX) return false;
         if (!fir_os_supported(sk, tk, K, D)) return false;
         return true;  // AUTO or OVERLAP_SAVE
     }
@@ -144,7 +157,16 @@ struct FirCore {
         p.nch = (int)nch;
         p.force_naive = 0;
         int st = SDRGPU_ERR_UNSUPPORTED;
-        if (want_os()) {
+        if (want_mx()) {
+            if (!mx_state && mx_status == SDRGPU_OK)
+                mx_state = fir_mx_prepare(device, reinterpret_cast<const float*>(taps_host.data()),
+                                          K, D, &mx_status);
+            if (mx_state) st = fir_mx_launch(p, mx_state, stream.cur);
+            else if (mx_status != SDRGPU_ERR_UNSUPPORTED) return mx_status;
+            // an unaligned buffer (UNSUPPORTED) falls through to the other paths
+            if (st != SDRGPU_OK && st != SDRGPU_ERR_UNSUPPORTED) return st;
+        }
+        if (st != SDRGPU_OK && want_os()) {
             if (!os_state && os_status == SDRGPU_OK)
                 os_state = fir_os_prepare(device, sk, tk, taps_host.data(), K, D, stream.cur,
                                           &os_status);
@@ -226,9 +248,12 @@ int sdrgpu_fir_create(int device, int sample_kind, int tap_kind, const void* tap
 }
 
 int sdrgpu_fir_set_algorithm(sdrgpu_fir* h, int algo) {
-    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_OVERLAP_SAVE) return SDRGPU_ERR_INVALID;
+    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_MATRIX) return SDRGPU_ERR_INVALID;
     if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
         !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        return SDRGPU_ERR_UNSUPPORTED;
+    if (algo == SDRGPU_FIR_MATRIX &&
+        !fir_mx_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     h->core.algo = algo;
     return SDRGPU_OK;
@@ -320,9 +345,12 @@ int sdrgpu_firbank_create(int device, int sample_kind, int tap_kind, const void*
 }
 
 int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo) {
-    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_OVERLAP_SAVE) return SDRGPU_ERR_INVALID;
+    if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_MATRIX) return SDRGPU_ERR_INVALID;
     if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
         !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        return SDRGPU_ERR_UNSUPPORTED;
+    if (algo == SDRGPU_FIR_MATRIX &&
+        !fir_mx_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     h->core.algo = algo;
     return SDRGPU_OK;

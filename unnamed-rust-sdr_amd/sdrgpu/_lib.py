@@ -27,6 +27,7 @@ C64 = 1
 FIR_AUTO = 0
 FIR_DIRECT = 1
 FIR_OVERLAP_SAVE = 2
+FIR_MATRIX = 3
 
 BQ_IDENTITY = 0
 BQ_LOWPASS = 1
