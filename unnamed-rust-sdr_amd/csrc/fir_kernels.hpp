@@ -44,4 +44,11 @@ int fir_direct2_launch(const FirParams& p, hipStream_t s);
 struct FirOsPlan;
 int fir_os_supported(int sample_kind, int tap_kind, int K, int D);
 
+// LDS-staged split-bf16 MFMA direct form (fir_mxl.hip): c64 samples, f32 taps, D = 4,
+// K <= 385, 16-byte aligned input.  d_dummy: fir_mxl_dummy_bytes() of readable memory.
+int fir_mxl_supported(const FirParams& p);
+size_t fir_mxl_dummy_bytes();
+int fir_mxl_launch(const FirParams& p, const float* d_taps, const void* d_dummy, int cus,
+                   hipStream_t s);
+
 }  // namespace sdrgpu

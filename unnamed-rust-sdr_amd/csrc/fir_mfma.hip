@@ -282,6 +282,7 @@ void fir_mx_kernel(MxParams p) {
 struct MxState {
     int K = 0, D = 0, NCH = 0;
     float* d_taps = nullptr;
+    void* d_dummy = nullptr;  // zeroed target of fir_mxl's clamped prefetches
     int cus = 256;
 };
 
@@ -318,8 +319,11 @@ void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status) {
         cus > 0)
         st->cus = cus;
     if (hipMalloc(&st->d_taps, sizeof(float) * K) != hipSuccess ||
-        hipMemcpy(st->d_taps, taps, sizeof(float) * K, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(st->d_taps, taps, sizeof(float) * K, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&st->d_dummy, fir_mxl_dummy_bytes()) != hipSuccess ||
+        hipMemset(st->d_dummy, 0, fir_mxl_dummy_bytes()) != hipSuccess) {
         if (st->d_taps) (void)hipFree(st->d_taps);
+        if (st->d_dummy) (void)hipFree(st->d_dummy);
         delete st;
         if (status) *status = SDRGPU_ERR_NOMEM;
         return nullptr;
@@ -332,6 +336,7 @@ void fir_mx_release(void* state) {
     auto* st = static_cast<MxState*>(state);
     if (!st) return;
     if (st->d_taps) (void)hipFree(st->d_taps);
+    if (st->d_dummy) (void)hipFree(st->d_dummy);
     delete st;
 }
 
@@ -340,6 +345,14 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
         fp.K != st->K)
         return SDRGPU_ERR_UNSUPPORTED;
+    // default for D = 4: the LDS-staged kernel (fir_mxl.hip); SDRGPU_MX_VARIANT=1 keeps
+    // the register-fed kernel below for A/B
+    static const int variant = [] {
+        const char* e = getenv("SDRGPU_MX_VARIANT");
+        return e ? atoi(e) : 2;
+    }();
+    if (variant != 1 && fir_mxl_supported(fp))
+        return fir_mxl_launch(fp, st->d_taps, st->d_dummy, st->cus, s);
     // 16-byte loads of sample pairs: channel bases must stay 16-byte aligned
     if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
         return SDRGPU_ERR_UNSUPPORTED;
