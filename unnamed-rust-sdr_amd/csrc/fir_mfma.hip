@@ -33,6 +33,7 @@
 // 16 segments per wave, one 256-lane workgroup per CU.  Algorithmic bytes per input sample
 // at D=4: 8 in + 2 out = 10 B; MFMA work 6 x (K+15D rounded to 32) / (16 x 16) per output.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "fir_kernels.hpp"
@@ -283,6 +284,7 @@ struct MxState {
     int K = 0, D = 0, NCH = 0;
     float* d_taps = nullptr;
     void* d_dummy = nullptr;  // zeroed target of fir_mxl's clamped prefetches
+    int tap_scale_exp = 0;    // fir_mxh: 15 - exponent(max |h|)
     int cus = 256;
 };
 
@@ -314,6 +316,13 @@ void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status) {
     st->K = K;
     st->D = D;
     st->NCH = mx_nch(K, D);
+    {
+        float hmax = 0.f;
+        for (int k = 0; k < K; ++k) hmax = std::max(hmax, std::fabs(taps[k]));
+        int e = 0;
+        (void)std::frexp(hmax, &e);
+        st->tap_scale_exp = std::min(126, std::max(-126, 15 - e));
+    }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
@@ -345,13 +354,16 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
         fp.K != st->K)
         return SDRGPU_ERR_UNSUPPORTED;
-    // default for D = 4: the LDS-staged kernel (fir_mxl.hip); SDRGPU_MX_VARIANT=1 keeps
-    // the register-fed kernel below for A/B
+    // D = 4: the LDS-staged kernels -- fp16 two-way split at two waves per SIMD
+    // (fir_mxh.hip, default), bf16 three-way split at one (fir_mxl.hip, K <= 385 and
+    // SDRGPU_MX_VARIANT=2); SDRGPU_MX_VARIANT=1 keeps the register-fed kernel below.
     static const int variant = [] {
         const char* e = getenv("SDRGPU_MX_VARIANT");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : 3;
     }();
-    if (variant != 1 && fir_mxl_supported(fp))
+    if (variant == 3 && fir_mxh_supported(fp))
+        return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
+    if (variant >= 2 && fir_mxl_supported(fp))
         return fir_mxl_launch(fp, st->d_taps, st->d_dummy, st->cus, s);
     // 16-byte loads of sample pairs: channel bases must stay 16-byte aligned
     if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))

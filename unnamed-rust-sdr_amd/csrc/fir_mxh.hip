@@ -1,0 +1,442 @@
+// fir_mxh.hip -- LDS-staged MFMA direct-form FIR, decimate by 4, on a per-tile scaled
+// two-way fp16 split (gfx950): two waves per SIMD.
+//
+// Semantics: Fir::apply + Decimate (reference src/filter/fir.rs:23-32,
+// src/filter/convolve.rs:13-15, src/signal/adapters/mod.rs:30-37) for complex samples and
+// real taps: y[m] = sum_k h[k] x[i0 + 4m - k], zero history before the stream start.
+//
+// Same GEMM shape, tiles and conflict-free LDS swizzle as fir_mxl.hip (read that header
+// first); what changes is the operand format, which halves both the MFMA work and the
+// LDS footprint so that two waves share each SIMD (one's VALU/LDS staging and memory waits
+// overlap the other's MFMAs):
+//   * every tile's window (1024 new samples + H history samples) is staged with its own
+//     power-of-two scale 2^s, s = 15 - exponent(max |x| over the window), so the scaled
+//     samples lie below 2^15 and fit fp16; each scaled sample is split into
+//     xh = rtz_f16(x) and xl = rtz_f16(x - xh) (x is represented to < 2^-20 relative);
+//   * taps likewise: h 2^sh = hh + hl (round-to-nearest, host-chosen sh);
+//   * x h ~= xh hh + xh hl + xl hh on v_mfma_f32_16x16x32_f16 (3 MFMAs per component
+//     instead of the bf16 path's 6; the dropped xl hl < 2^-20 |x h|), and the tile's
+//     outputs are rescaled by 2^-(s + sh) before the store.
+// The scale is per tile, so a sample's relative precision is 2^-20 of the largest sample
+// within the same ~1280-sample window (the reference's own f32 sum has a rounding error of
+// 2^-24 of its largest term); samples more than 2^-24 below that maximum (or |x| < 2^-111)
+// fall into fp16 subnormals.  f32's exponent range is otherwise kept (any input scale).
+//
+// LDS per wave: two window buffers (tile t computes from one while tile t+1 is staged into
+// the other -- no aliasing, no ordering constraints), each 4 planes (hi/lo x re/im) of
+// H + 1024 bf16-sized samples: 2 x 4 x 1280 x 2 B = 20 KiB at NCH = 10, so 8 waves fill the
+// 160 KiB of a CU exactly.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "fir_kernels.hpp"
+
+namespace sdrgpu {
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kD = 4;
+constexpr int kTileOut = 256;
+constexpr int kTileIn = kTileOut * kD;  // 1024 new samples per tile
+constexpr int kWaves = 8;               // two waves per SIMD
+constexpr int kBlock = 64 * kWaves;
+
+template <int NCH>
+struct GeoH {
+    static constexpr int H = 32 * NCH - 16 * kD;  // history samples of a tile's window
+    static constexpr int WL = H + kTileIn;        // window samples
+    static constexpr int PLB = 2 * WL;            // bytes per plane
+    static constexpr int WINB = 4 * PLB;          // bytes per window buffer
+    static constexpr int WAVE = 2 * WINB;         // bytes per wave
+    static constexpr int NH = H / 128;            // history groups
+    static constexpr int KH = 8 - NH;             // first tile group that is next history
+    static_assert(H % 128 == 0 && H > 0 && H < kTileIn, "geometry");
+    static_assert(kWaves * WAVE <= 160 * 1024, "LDS");
+};
+
+struct MxhParams {
+    const float2* in;
+    long ld_in, n_in;
+    const float2* hist;
+    float2* hist_next;
+    const float2* dummy;  // >= 1024 readable samples: target of clamped prefetches
+    long n_out;
+    int K;
+    int delta;  // 3 - i0
+    int sh;     // tap scale exponent
+    const float* taps;
+    float2* out;
+    long ld_out;
+    long tpc, spc, seg_tiles, units;
+    int vec_out;
+};
+
+__device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ unsigned pk_rtz(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+
+__device__ __forceinline__ float lo_f(unsigned u) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu));
+}
+__device__ __forceinline__ float hi_f(unsigned u) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16));
+}
+
+// (a, b) already scaled: packed fp16 hi = rtz(x), lo = rtz(x - hi)
+__device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
+    hi = pk_rtz(a, b);
+    lo = pk_rtz(a - lo_f(hi), b - hi_f(hi));
+}
+
+__device__ __forceinline__ int sigma(int v) {
+    return v < 4 ? 2 * v : (v >= 12 ? 2 * v - 16 : 2 * v - 7);
+}
+
+__device__ __forceinline__ float2 fetch1(const float2* in, const float2* hist, long j, long n_in,
+                                         int K) {
+    const bool inb = (j >= 0) & (j < n_in);
+    const bool inh = (j < 0) & (j >= -(long)(K - 1));
+    const float2 xa = in[inb ? j : 0];
+    const float2 xb = hist[inh ? j + (K - 1) : 0];
+    return inb ? xa : (inh ? xb : make_float2(0.f, 0.f));
+}
+
+__device__ __forceinline__ float4 fetch_pair(const float2* in, const float2* hist, long j,
+                                             long n_in, int K) {
+    const float2 a = fetch1(in, hist, j, n_in, K), b = fetch1(in, hist, j + 1, n_in, K);
+    return make_float4(a.x, a.y, b.x, b.y);
+}
+
+__device__ __forceinline__ void st32(char* lds, int a, unsigned v) {
+    *reinterpret_cast<unsigned*>(lds + a) = v;
+}
+
+// scale + split one sample pair into the 4 planes (re hi, re lo, im hi, im lo) at byte a
+template <int PLB>
+__device__ __forceinline__ void put_pair(char* lds, int a, const float4& f, float sc) {
+    unsigned h, l;
+    split2(f.x * sc, f.z * sc, h, l);
+    st32(lds, a, h);
+    st32(lds, a + PLB, l);
+    split2(f.y * sc, f.w * sc, h, l);
+    st32(lds, a + 2 * PLB, h);
+    st32(lds, a + 3 * PLB, l);
+}
+
+__device__ __forceinline__ float absmax4(float m, const float4& f) {
+    return fmaxf(fmaxf(m, fmaxf(fabsf(f.x), fabsf(f.y))), fmaxf(fabsf(f.z), fabsf(f.w)));
+}
+
+// window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float
+__device__ __forceinline__ int wave_scale(float m) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    int s = 15 - __builtin_amdgcn_frexp_expf(m);
+    s = s < -126 ? -126 : (s > 126 ? 126 : s);
+    return __builtin_amdgcn_readfirstlane(s);
+}
+
+__device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1.0f, s); }
+
+// ABL (debug ablation, results invalid): 1 = memory only (no LDS reads / MFMA),
+// 2 = no HBM loads (compute only)
+// NT: bit 0 = non-temporal sample loads, bit 1 = non-temporal output stores
+template <int NCH, int ABL = 0, int NT = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void fir_mxh_kernel(MxhParams p) {
+    using G = GeoH<NCH>;
+    constexpr int H = G::H, PLB = G::PLB, WINB = G::WINB, NH = G::NH, KH = G::KH;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const long wave = (long)blockIdx.x * kWaves + wv;
+    const long nwaves = (long)gridDim.x * kWaves;
+    const int g = lane >> 4, v = lane & 15;
+    const int K = p.K;
+    const int base = wv * G::WAVE;
+
+    // ---- A: scaled tap Toeplitz fragments (fp16 hi / lo) ----
+    u32x4 ah[NCH], al[NCH];
+    {
+        const float tsc = exp2i(p.sh);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                unsigned hw = 0, lw = 0;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int pidx = 32 * c + 8 * g + 2 * jj + e;
+                    const int k = 4 * v + 3 - p.delta + H - pidx;
+                    const bool ok = (k >= 0) & (k < K);
+                    const float hk = p.taps[ok ? k : 0];
+                    const float hs = ok ? hk * tsc : 0.f;
+                    const _Float16 h16 = (_Float16)hs;
+                    const _Float16 l16 = (_Float16)(hs - (float)h16);
+                    hw |= (unsigned)__builtin_bit_cast(unsigned short, h16) << (16 * e);
+                    lw |= (unsigned)__builtin_bit_cast(unsigned short, l16) << (16 * e);
+                }
+                ah[c][jj] = hw;
+                al[c][jj] = lw;
+            }
+        }
+    }
+
+    const int sv = sigma(v);
+    int rb[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int r = sv + (c >> 1);
+        rb[c] = base + 128 * r + 16 * ((4 * (c & 1) + g) ^ ((r >> 1) & 7));
+    }
+    const int wb0 = base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7);
+
+    for (long u = wave; u < p.units; u += nwaves) {
+        const long ch = u / p.spc;
+        const long t0 = (u - ch * p.spc) * p.seg_tiles;
+        const long nt = std::min(p.seg_tiles, p.tpc - t0);
+        if (nt <= 0) continue;
+        const float2* __restrict__ in = p.in + ch * p.ld_in;
+        const float2* __restrict__ hist = p.hist + ch * (long)(K - 1);
+        float2* __restrict__ out = p.out + ch * p.ld_out;
+        const long n_in = p.n_in;
+        const long N0 = (long)kTileIn * t0;
+        long ntf = (n_in - N0) / kTileIn;
+        ntf = n_in < N0 ? 0 : (ntf > nt ? nt : ntf);
+
+        auto ldx = [&](const float2* q) {
+            const f32x4* q4 = reinterpret_cast<const f32x4*>(q);
+            const f32x4 r = (NT & 1) ? __builtin_nontemporal_load(q4) : *q4;
+            return make_float4(r[0], r[1], r[2], r[3]);
+        };
+        auto load_tile = [&](float4 (&dst)[8], long t) {
+            const long j0 = N0 + (long)kTileIn * t;
+            if (ABL == 2) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    dst[k] = make_float4((float)(j0 + k), 1.f, 2.f, (float)lane);
+                return;
+            }
+            if (t < ntf) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    dst[k] = ldx(in + j0 + 128 * k + 2 * lane);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    dst[k] = fetch_pair(in, hist, j0 + 128 * k + 2 * lane, n_in, K);
+            }
+        };
+        auto window_scale = [&](const float4 (&nx)[8], const float4 (&hr)[NH]) {
+            float m = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) m = absmax4(m, nx[k]);
+#pragma unroll
+            for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
+            return wave_scale(m);
+        };
+        auto hist_addr = [&](int k) { return (wb0 ^ (16 * (k & 7))) + 256 * k; };
+        auto new_addr = [&](int k) {
+            return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
+        };
+
+        float4 ra[8], hr[NH];  // one raw tile in flight per wave (two waves per SIMD)
+#pragma unroll
+        for (int k = 0; k < NH; ++k)
+            hr[k] = fetch_pair(in, hist, N0 - H + 128 * k + 2 * lane, n_in, K);
+        load_tile(ra, 0);
+        int s_cur = window_scale(ra, hr);
+        {
+            const float sc = exp2i(s_cur);
+#pragma unroll
+            for (int k = 0; k < NH; ++k) put_pair<PLB>(smem, hist_addr(k), hr[k], sc);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) put_pair<PLB>(smem, new_addr(k), ra[k], sc);
+#pragma unroll
+            for (int k = 0; k < NH; ++k) hr[k] = ra[KH + k];
+        }
+        if (nt > 1) load_tile(ra, 1);
+
+        auto body = [&](auto tau_c, long t, float4 (&nx)[8]) {
+            constexpr int TAU = decltype(tau_c)::value;
+            constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
+            const bool fast2 = t + 2 < ntf;
+            const float2* src2 = fast2 ? in + N0 + (long)kTileIn * (t + 2) : p.dummy;
+            const int s_next = window_scale(nx, hr);
+            const float scn = exp2i(s_next);
+            f32x4 cr = {0.f, 0.f, 0.f, 0.f}, ci = {0.f, 0.f, 0.f, 0.f};
+            u32x4 fb[2][4];
+            auto read_frags = [&](u32x4 (&f)[4], int c) {
+                const int a = rb[c] + TAU * WINB;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
+            };
+            if (ABL != 1) read_frags(fb[0], 0);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                if (ABL != 1) {
+                    if (c + 1 < NCH) read_frags(fb[(c + 1) & 1], c + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const u32x4(&f)[4] = fb[c & 1];
+                    cr = mfma(al[c], f[0], cr);
+                    ci = mfma(al[c], f[2], ci);
+                    cr = mfma(ah[c], f[1], cr);
+                    ci = mfma(ah[c], f[3], ci);
+                    cr = mfma(ah[c], f[0], cr);
+                    ci = mfma(ah[c], f[2], ci);
+                }
+                if (c == 0) {  // next window's history = this tile's tail (old hr)
+#pragma unroll
+                    for (int k = 0; k < NH; ++k)
+                        put_pair<PLB>(smem, WN + hist_addr(k), hr[k], scn);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if ((k < NCH - 1 ? k : NCH - 1) != c) continue;
+                    put_pair<PLB>(smem, WN + new_addr(k), nx[k], scn);
+                    if (k >= KH) hr[k - KH] = nx[k];
+                    if (ABL != 2)
+                        nx[k] = ldx(src2 + 128 * k + 2 * lane);
+                }
+            }
+            if (!fast2 && t + 2 < nt) load_tile(nx, t + 2);
+            const int so = -(s_cur + p.sh);
+            const long m = (t0 + t) * kTileOut + 16 * sv + 4 * g;
+            float yr[4], yi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                yr[i] = __builtin_amdgcn_ldexpf(cr[i], so);
+                yi[i] = __builtin_amdgcn_ldexpf(ci[i], so);
+            }
+            if (p.vec_out && (t0 + t + 1) * kTileOut <= p.n_out) {
+                f32x4* o4 = reinterpret_cast<f32x4*>(out + m);
+                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                if (NT & 2) {
+                    __builtin_nontemporal_store(y0, o4);
+                    __builtin_nontemporal_store(y1, o4 + 1);
+                } else {
+                    o4[0] = y0;
+                    o4[1] = y1;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+            }
+            s_cur = s_next;
+        };
+
+        for (long t = 0; t < nt; t += 2) {
+            body(std::integral_constant<int, 0>(), t, ra);
+            if (t + 1 >= nt) break;
+            body(std::integral_constant<int, 1>(), t + 1, ra);
+        }
+    }
+
+    if (blockIdx.x == gridDim.x - 1 && p.hist_next) {  // stream history carry
+        const long nch = p.units / p.spc;
+        for (long j = threadIdx.x; j < nch * (K - 1); j += kBlock) {
+            const long ch = j / (K - 1), jj = j - ch * (K - 1);
+            const float2* inc = p.in + ch * p.ld_in;
+            const float2* hic = p.hist + ch * (long)(K - 1);
+            const long gidx = p.n_in - (long)(K - 1) + jj;
+            p.hist_next[j] = gidx >= 0 ? inc[gidx] : hic[gidx + (K - 1)];
+        }
+    }
+}
+
+int mxh_nch(int K) {
+    const int need = (K + 63 + 31) / 32;  // 32 NCH >= K + 15*4 + 3
+    if (need <= 6) return 6;
+    if (need <= 10) return 10;
+    return 0;
+}
+
+}  // namespace
+
+int fir_mxh_supported(const FirParams& fp) {
+    if (fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != kD) return 0;
+    if (fp.K < 1 || mxh_nch(fp.K) == 0) return 0;
+    if (fp.i0 < 0 || fp.i0 >= kD) return 0;
+    if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
+        return 0;
+    return 1;
+}
+
+int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
+                   const void* d_dummy, int cus, hipStream_t s) {
+    if (!fir_mxh_supported(fp) || !d_dummy) return SDRGPU_ERR_UNSUPPORTED;
+    const int NCH = mxh_nch(fp.K);
+    MxhParams p;
+    p.in = static_cast<const float2*>(fp.in);
+    p.ld_in = fp.ld_in;
+    p.n_in = fp.n_in;
+    p.hist = static_cast<const float2*>(fp.hist);
+    p.hist_next = fp.K > 1 ? static_cast<float2*>(fp.hist_next) : nullptr;
+    p.dummy = static_cast<const float2*>(d_dummy);
+    p.n_out = fp.n_out;
+    p.K = fp.K;
+    p.delta = (int)(kD - 1 - fp.i0);
+    p.sh = tap_scale_exp;
+    p.taps = d_taps;
+    p.out = static_cast<float2*>(fp.out);
+    p.ld_out = fp.ld_out;
+    p.vec_out = ((reinterpret_cast<uintptr_t>(fp.out) & 15) == 0 &&
+                 (fp.nch == 1 || !(fp.ld_out & 1)))
+                    ? 1
+                    : 0;
+    const long nch = fp.nch;
+    p.tpc = ceil_div(std::max(0L, fp.n_out), kTileOut);
+    const long W = (long)kWaves * cus;
+    long spc = nch >= W ? 1 : ceil_div(W, nch);
+    spc = std::max(1L, std::min(spc, p.tpc));
+    p.seg_tiles = std::max(1L, ceil_div(p.tpc, spc));
+    static const long seg_env = [] {
+        const char* e = getenv("SDRGPU_MXL_SEG");
+        return e ? atol(e) : 0L;
+    }();
+    if (seg_env > 0) p.seg_tiles = std::min(p.seg_tiles, seg_env);
+    p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
+    p.units = nch * p.spc;
+    const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
+    static const char* abl_env = getenv("SDRGPU_MX_ABLATION");
+    const int abl = abl_env ? atoi(abl_env) : 0;
+    static const int nt = [] {
+        const char* e = getenv("SDRGPU_MXH_NT");  // default: both non-temporal (streamed once)
+        return e ? atoi(e) : 3;
+    }();
+#define SDRGPU_MXH_GO(CC, A, N)                                                                 \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, A, N>), dim3(blocks), dim3(kBlock),                 \
+                       (size_t)kWaves * GeoH<CC>::WAVE, s, p)
+#define SDRGPU_MXH_CASE(CC)                                                                    \
+    if (NCH == CC) {                                                                           \
+        if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0);                                                 \
+        else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 0);                                            \
+        else if (nt == 1) SDRGPU_MXH_GO(CC, 0, 1);                                             \
+        else if (nt == 2) SDRGPU_MXH_GO(CC, 0, 2);                                             \
+        else if (nt == 3) SDRGPU_MXH_GO(CC, 0, 3);                                             \
+        else SDRGPU_MXH_GO(CC, 0, 0);                                                          \
+        SDRGPU_LAUNCH_CHECK();                                                                 \
+        return SDRGPU_OK;                                                                      \
+    }
+    SDRGPU_MXH_CASE(10)
+    SDRGPU_MXH_CASE(6)
+#undef SDRGPU_MXH_CASE
+#undef SDRGPU_MXH_GO
+    return SDRGPU_ERR_UNSUPPORTED;
+}
+
+}  // namespace sdrgpu
