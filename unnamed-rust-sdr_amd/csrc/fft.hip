@@ -18,6 +18,7 @@
 // Roofline: HBM bound (C3: 24 algorithmic bytes per input sample, ~160 flop), see DESIGN.md.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "fft_device.hpp"
@@ -244,6 +245,132 @@ __global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
     }
 }
 
+
+// -------- 65536-point four-step (256 x 256) with wide LDS tiles ---------------------------
+// n = 256 r + col, k = k1 + 256 k2.  Pass A: for CB columns per workgroup, FFT-256 over r
+// (r = j + 16 m: DFT16 over m in registers, x W_256^{j ka}, LDS transpose, DFT16 over j),
+// x W_65536^{col k1}, store S[k1][col] (lanes walk col).  Pass B: for CB consecutive k1
+// per workgroup, rows S[k1][*] are read contiguously into LDS, FFT-256 over col the same
+// way, and the collated output rows are written with lanes walking k1 (8*CB bytes per k2).
+// Global accesses are 8*CB-byte runs (the generic path above moves 128-byte runs); LDS
+// accesses are conflict-free (8-byte lanes, padded row pitch in B).
+// CB = columns (pass A) / k1 rows (pass B) per workgroup: 16*CB lanes, each lane one
+// (j, column) pair; CB = 32 -> 64 KiB (A) / 66 KiB (B) of LDS, two workgroups per CU.
+struct F64Args {
+    FrameSrc src;
+    long nframes;
+    const float2* tw;   // W_4096
+    const float2* twM;  // W_65536
+    float norm;
+    float2* scratch;
+    float2* out;
+};
+
+template <typename T> __device__ __forceinline__ T ld_nt(const T* p) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 r = __builtin_nontemporal_load(reinterpret_cast<const f2*>(p));
+    return make_float2(r[0], r[1]);
+}
+__device__ __forceinline__ void st_nt(float2* p, float2 v) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 r = {v.x, v.y};
+    __builtin_nontemporal_store(r, reinterpret_cast<f2*>(p));
+}
+
+// NT: non-temporal hint on the streamed frame loads (pass A) and output stores (pass B), so
+// the stream does not evict the MALL-resident scratch slab
+template <int CB, bool NT>
+__global__ __launch_bounds__(16 * CB) void fft64k_pass_a(F64Args a) {
+    __shared__ float2 lds[16 * 16 * CB];
+    constexpr long M = 65536;
+    constexpr int NB = 256 / CB;  // workgroups per frame
+    const int c = threadIdx.x % CB, j = threadIdx.x / CB;
+    const long f = blockIdx.x / NB;
+    const int col = CB * (int)(blockIdx.x % NB) + c;
+    if (f >= a.nframes) return;
+    float2 v[16];
+    // frame f samples n = 256 (j + 16 m) + col
+    const FrameSrc& s = a.src;
+    long g0 = 0;
+    bool fast = s.mode == 0;
+    if (s.mode == 1) {
+        g0 = s.first_end + f * s.hop - M;
+        fast = g0 >= 0 && g0 + M <= s.n_in;
+    }
+    if (fast) {
+        const float2* src = s.mode == 0 ? s.in + f * M : s.in + g0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            v[m] = NT ? ld_nt(src + 256 * (j + 16 * m) + col) : src[256 * (j + 16 * m) + col];
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = frame_sample(s, M, f, 256 * (j + 16 * m) + col);
+    }
+    Dft<16, false>::run(v);
+    if (j) twiddle<16, false>(v, a.tw, 16 * j);
+#pragma unroll
+    for (int ka = 0; ka < 16; ++ka) lds[(ka * 16 + j) * CB + c] = v[ka];
+    __syncthreads();
+    const int ka = j;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = lds[(ka * 16 + jj) * CB + c];
+    Dft<16, false>::run(v);
+    // v[kb] = column FFT at k1 = ka + 16 kb; x W_65536^{col k1} = W^{col ka} (W_4096^{col})^kb
+    const float2 w1 = a.twM[col * ka];
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) v[kb] = cmul(v[kb], w1);
+    twiddle<16, false>(v, a.tw, col);
+    float2* S = a.scratch + f * M;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) S[(long)(ka + 16 * kb) * 256 + col] = v[kb];
+}
+
+template <int CB, bool NT>
+__global__ __launch_bounds__(16 * CB) void fft64k_pass_b(F64Args a) {
+    constexpr int P = CB + 1;  // LDS row pitch (float2): conflict-free transposes
+    __shared__ float2 lds[256 * P];
+    constexpr long M = 65536;
+    constexpr int NB = 256 / CB;
+    constexpr int NTH = 16 * CB;
+    const int t = threadIdx.x;
+    const long f = blockIdx.x / NB;
+    const int k1b = CB * (int)(blockIdx.x % NB);
+    if (f >= a.nframes) return;
+    const float2* S = a.scratch + f * M + (long)k1b * 256;
+    // rows k1b + r (r < CB), 256 columns each: coalesced, transposed into lds[col][r]
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int p = t + NTH * i;
+        const int r = p >> 8, col = p & 255;
+        lds[col * P + r] = S[p];
+    }
+    __syncthreads();
+    const int r = t % CB, j = t / CB;
+    float2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = lds[(j + 16 * m) * P + r];
+    __syncthreads();
+    Dft<16, false>::run(v);
+    if (j) twiddle<16, false>(v, a.tw, 16 * j);
+#pragma unroll
+    for (int ka = 0; ka < 16; ++ka) lds[(ka * 16 + j) * P + r] = v[ka];
+    __syncthreads();
+    const int ka = j;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = lds[(ka * 16 + jj) * P + r];
+    Dft<16, false>::run(v);
+    // X[k1 + 256 k2] with k1 = k1b + r, k2 = ka + 16 kb -> collated out[(k + M/2) mod M]
+    float2* O = a.out + f * M;
+    const float nrm = a.norm;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) {
+        const int k2 = (ka + 16 * kb + 128) & 255;
+        const float2 y = make_float2(v[kb].x * nrm, v[kb].y * nrm);
+        if (NT) st_nt(O + (long)k2 * 256 + k1b + r, y);
+        else O[(long)k2 * 256 + k1b + r] = y;
+    }
+}
+
 }  // namespace
 
 // ------------------------------ plan / launch -------------------------------------------
@@ -306,9 +433,14 @@ int fft_plan_size(void* plan) { return static_cast<FftPlanDev*>(plan)->M; }
 size_t fft_scratch_frames(void* plan) {
     auto* p = static_cast<FftPlanDev*>(plan);
     if (p->M <= kTile) return 0;
-    // keep the slab around 64 MiB so pass B reads it from the MALL
+    // scratch slab of ~256 MiB (the MALL size): 512 workgroups per pass, 32 launches per 2^28
+    // samples; measured 2.79 ms vs 2.92 (128 MiB), 3.08 (64 MiB), 3.23 (512 MiB)
+    static const size_t mib = [] {
+        const char* e = getenv("SDRGPU_FFT_SLAB_MIB");
+        return (size_t)(e ? atoi(e) : 256);
+    }();
     const size_t per = (size_t)p->M * sizeof(float2);
-    return std::max<size_t>(1, (64u << 20) / per);
+    return std::max<size_t>(1, (mib << 20) / per);
 }
 
 int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
@@ -354,6 +486,53 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         return SDRGPU_OK;
     }
     if (store_mode != 0 || !scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
+    static const bool use64 = [] {
+        const char* e = getenv("SDRGPU_FFT64K");
+        return !e || atoi(e) != 0;
+    }();
+    if (p->M == 65536 && use64) {
+        static const int cb = [] {
+            const char* e = getenv("SDRGPU_FFT64K_CB");
+            return e && atoi(e) == 64 ? 64 : 32;
+        }();
+        static const bool nt = [] {
+            const char* e = getenv("SDRGPU_FFT64K_NT");
+            return !e || atoi(e) != 0;
+        }();
+        F64Args a{};
+        a.tw = p->tw4096;
+        a.twM = p->twM;
+        a.norm = p->norm;
+        a.scratch = scratch;
+        for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
+            const long nf = std::min((long)scratch_frames, fr.nframes - f0);
+            a.src = src;
+            if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
+            else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
+            a.nframes = nf;
+            a.out = out + f0 * (long)p->M;
+            const dim3 g((unsigned)(nf * (256 / cb))), b(16 * cb);
+            if (cb == 64 && nt) {
+                hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, s, a);
+                SDRGPU_LAUNCH_CHECK();
+                hipLaunchKernelGGL((fft64k_pass_b<64, true>), g, b, 0, s, a);
+            } else if (cb == 64) {
+                hipLaunchKernelGGL((fft64k_pass_a<64, false>), g, b, 0, s, a);
+                SDRGPU_LAUNCH_CHECK();
+                hipLaunchKernelGGL((fft64k_pass_b<64, false>), g, b, 0, s, a);
+            } else if (nt) {
+                hipLaunchKernelGGL((fft64k_pass_a<32, true>), g, b, 0, s, a);
+                SDRGPU_LAUNCH_CHECK();
+                hipLaunchKernelGGL((fft64k_pass_b<32, true>), g, b, 0, s, a);
+            } else {
+                hipLaunchKernelGGL((fft64k_pass_a<32, false>), g, b, 0, s, a);
+                SDRGPU_LAUNCH_CHECK();
+                hipLaunchKernelGGL((fft64k_pass_b<32, false>), g, b, 0, s, a);
+            }
+            SDRGPU_LAUNCH_CHECK();
+        }
+        return SDRGPU_OK;
+    }
     FourArgs a{};
     a.M = p->M;
     a.M1 = p->M1;
