@@ -59,8 +59,10 @@ enum sdrgpu_fir_algo {
     SDRGPU_FIR_AUTO = 0,          /* pick per shape */
     SDRGPU_FIR_DIRECT = 1,        /* LDS-tiled direct form, register-blocked outputs */
     SDRGPU_FIR_OVERLAP_SAVE = 2,  /* polyphase overlap-save, LDS-resident FFT tiles */
-    SDRGPU_FIR_MATRIX = 3,        /* direct form on bf16 MFMA with an exact 3-way f32 split
-                                     (c64 samples, f32 taps, decim 2/4/8, 16-B aligned input) */
+    SDRGPU_FIR_MATRIX = 3,        /* direct form on the 16-bit MFMAs with an f32-accurate operand
+                                     split: per-tile scaled fp16 x2 (decim 4, ntaps <= 257) or
+                                     exact bf16 x3 (decim 2/8); c64 samples, f32 taps, 16-B
+                                     aligned input.  AUTO picks it for those shapes. */
 };
 
 const char* sdrgpu_strerror(int code);   /* resample::Error Display, src/resample.rs:209-269 */
