@@ -11,6 +11,8 @@ per config:
       1024 channels x 2^20 c64                              PLL = loop-carried latency
   c5  255-tap FIR bank, channels sharded across GPUs,      16 B / input sample, HBM roof
       8192 channels x 2^16 c64 (1024 per GPU at 8 GPUs)
+  c2u8  configs[1] fed from rtl_tcp u8 IQ:    2 B in + 2 B out / sample
+      (v-128)/128 fused into the FIR load, 2^28 samples
 
 Multi-GPU (c5): `python -m torch.distributed.run --nproc-per-node N bench_configs.py
 --config c5`; each rank filters its resident channel shard (weak: 8192/N channels per rank
@@ -36,7 +38,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "all"])
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -114,6 +116,32 @@ def bench_c3(args):
                                "cores": 1, "kind": "proxy",
                                "sample": f"{done} NumPy pocketfft 64k frames (proxy for rustfft 3.0), {el:.1f} s"}
     return res
+
+
+# ------------------------------------------------------------------------------ c2u8
+def bench_c2u8(args):
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    n = 1 << 28
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    fir = sdrgpu.filter.Fir(taps, decim=4, sample_kind=sdrgpu.CU8).design(2.4e6)
+    pat = np.random.default_rng(21).integers(0, 256, size=2 * (1 << 22), dtype=np.uint8)
+    x = DeviceBuffer.empty(2 * n, np.uint8)
+    for off in range(0, 2 * n, pat.size):
+        x.upload(pat[:min(pat.size, 2 * n - off)], offset_bytes=off)
+    n_out = n // 4
+    y = DeviceBuffer.empty(n_out, np.complex64)
+
+    def step():
+        assert fir.process_dev(x.ptr, n, y.ptr, n_out) == n_out
+
+    wall, ms = time_events(step, fir.stream(), args.steps, args.warmup,
+                           lambda: (fir.sync(), synchronize()))
+    return {"config": "c2u8: configs[1] (255-tap FIR, decim 4) fed from rtl_tcp u8 IQ, "
+                      "(v-128)/128 fused into the load, 2^28 samples",
+            "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
+            "roofline": roof(2 + 8 / 4, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
 
 
 # ------------------------------------------------------------------------------ c4
@@ -235,9 +263,9 @@ def bench_c5(args):
 
 def main():
     args = parse()
-    todo = ["c3", "c4", "c5"] if args.config == "all" else [args.config]
+    todo = ["c3", "c4", "c5", "c2u8"] if args.config == "all" else [args.config]
     for c in todo:
-        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5}[c](args)
+        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8}[c](args)
         if r is not None:
             print(json.dumps(r), flush=True)
 

@@ -52,6 +52,11 @@ enum sdrgpu_status {
 enum sdrgpu_kind {
     SDRGPU_F32 = 0,  /* f32 */
     SDRGPU_C64 = 1,  /* num::Complex<f32> */
+    SDRGPU_CU8 = 2,  /* FIR input only: interleaved u8 I/Q as read from rtl_tcp
+                        (RtlTcpConnection::read, src/rtltcp.rs:136-140), converted to
+                        Complex<f32> as RtlTcpSignal::next does, (v - 128) / 128
+                        (src/rtltcp.rs:156-164), inside the FIR load; outputs are C64.
+                        1 sample = 2 bytes. */
 };
 
 /* FIR algorithm selection (results agree within the parity tolerance). */
@@ -100,8 +105,12 @@ int sdrgpu_event_destroy(void* event);
  * computes all and Decimate drops D-1 of every D; only the kept ones are computed here).
  * State (ntaps-1 history, decimation phase) carries across process() calls, so any
  * partition of a stream into blocks gives the same outputs.
- * Kinds: (F32,F32), (C64,F32), (C64,C64).  (F32 samples with C64 taps do not type-check
- * in the reference: f32 is not Mul<Complex<f32>, Output=f32>.)
+ * Kinds: (F32,F32), (C64,F32), (C64,C64), and (CU8,F32), (CU8,C64) for rtl_tcp u8 IQ
+ * (the reference's rtl.listen().filter(...) chain, examples/live.rs:29-31, src/main.rs:38-49):
+ * the (v-128)/128 conversion is fused into the FIR load (decim 4 with f32 taps runs on the
+ * MFMA path at 2 input bytes per sample); history and outputs are C64.
+ * (F32 samples with C64 taps do not type-check in the reference: f32 is not
+ * Mul<Complex<f32>, Output=f32>.)
  * ===================================================================================== */
 typedef struct sdrgpu_fir sdrgpu_fir;
 

@@ -68,7 +68,7 @@ struct StreamSlot {
     }
 };
 
-inline size_t kind_bytes(int kind) { return kind == SDRGPU_C64 ? 8 : 4; }
+inline size_t kind_bytes(int kind) { return kind == SDRGPU_C64 ? 8 : (kind == SDRGPU_CU8 ? 2 : 4); }
 
 }  // namespace detail
 }  // namespace sdrgpu

@@ -21,11 +21,13 @@ int fir_mx_supported(int sample_kind, int tap_kind, int K, int D);
 void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status);
 int fir_mx_launch(const FirParams& p, void* state, hipStream_t s);
 void fir_mx_release(void* state);
+int cu8_to_c64_launch(const void* in, long ld_in, long n, long nch, void* out, hipStream_t s);
 }  // namespace sdrgpu
 
 struct FirCore {
     int device = 0;
     int sk = SDRGPU_C64, tk = SDRGPU_F32;
+    int csk = SDRGPU_C64;  // compute kind: CU8 input is filtered as C64
     int K = 1, D = 1;
     size_t nch = 1;
     int algo = SDRGPU_FIR_AUTO;
@@ -36,14 +38,15 @@ struct FirCore {
     int cur = 0;
     unsigned long long seen = 0;           // stream samples consumed (decimation phase)
     StreamSlot stream;
-    DevBuf stage_in, stage_out;
+    DevBuf stage_in, stage_out, stage_conv;
     void* os_state = nullptr;              // overlap-save plan (lazily built)
     int os_status = SDRGPU_OK;
     void* mx_state = nullptr;              // split-bf16 MFMA direct-form plan (lazily built)
     int mx_status = SDRGPU_OK;
 
-    size_t sbytes() const { return kind_bytes(sk); }
-    size_t hist_bytes() const { return nch * (size_t)(K - 1) * sbytes(); }
+    size_t in_bytes() const { return kind_bytes(sk); }
+    size_t out_bytes() const { return kind_bytes(csk); }
+    size_t hist_bytes() const { return nch * (size_t)(K - 1) * out_bytes(); }
 
     long first_kept() const {
         const long g = (long)(seen % (unsigned long long)D);
@@ -63,6 +66,7 @@ struct FirCore {
         d_hist[0] = d_hist[1] = nullptr;
         stage_in.release();
         stage_out.release();
+        stage_conv.release();
         if (os_state) fir_os_release(os_state);
         os_state = nullptr;
         if (mx_state) fir_mx_release(mx_state);
@@ -89,12 +93,15 @@ struct FirCore {
             return SDRGPU_ERR_UNSUPPORTED;
         if (!((sample_kind == SDRGPU_F32 && tap_kind == SDRGPU_F32) ||
               (sample_kind == SDRGPU_C64 && tap_kind == SDRGPU_F32) ||
-              (sample_kind == SDRGPU_C64 && tap_kind == SDRGPU_C64)))
+              (sample_kind == SDRGPU_C64 && tap_kind == SDRGPU_C64) ||
+              (sample_kind == SDRGPU_CU8 && tap_kind == SDRGPU_F32) ||
+              (sample_kind == SDRGPU_CU8 && tap_kind == SDRGPU_C64)))
             return SDRGPU_ERR_INVALID;
         int st = check_device(dev);
         if (st) return st;
         device = dev;
         sk = sample_kind;
+        csk = sample_kind == SDRGPU_CU8 ? SDRGPU_C64 : sample_kind;
         tk = tap_kind;
         K = (int)ntaps;
         D = (int)decim;
@@ -121,12 +128,12 @@ struct FirCore {
 
     bool want_mx() const {
         if (algo != SDRGPU_FIR_AUTO && algo != SDRGPU_FIR_MATRIX) return false;
-        return fir_mx_supported(sk, tk, K, D) != 0;
+        return fir_mx_supported(csk, tk, K, D) != 0;
     }
 
     bool want_os() const {
         if (algo == SDRGPU_FIR_DIRECT || algo == SDRGPU_FIR_MATRIX) return false;
-        if (!fir_os_supported(sk, tk, K, D)) return false;
+        if (!fir_os_supported(csk, tk, K, D)) return false;
         return true;  // AUTO or OVERLAP_SAVE
     }
 
@@ -161,14 +168,30 @@ struct FirCore {
             if (!mx_state && mx_status == SDRGPU_OK)
                 mx_state = fir_mx_prepare(device, reinterpret_cast<const float*>(taps_host.data()),
                                           K, D, &mx_status);
-            if (mx_state) st = fir_mx_launch(p, mx_state, stream.cur);
+            if (mx_state) st = fir_mx_launch(p, mx_state, stream.cur);  // CU8: fused ingest
             else if (mx_status != SDRGPU_ERR_UNSUPPORTED) return mx_status;
             // an unaligned buffer (UNSUPPORTED) falls through to the other paths
             if (st != SDRGPU_OK && st != SDRGPU_ERR_UNSUPPORTED) return st;
         }
+        if (st != SDRGPU_OK && sk == SDRGPU_CU8) {
+            // not fused for this shape: convert the block to C64 (RtlTcpSignal::next), then
+            // filter it like any C64 block
+            if ((st = stage_conv.ensure(nch * n_in * sizeof(float) * 2))) return st;
+            if ((st = cu8_to_c64_launch(d_in, (long)ld_in, (long)n_in, (long)nch, stage_conv.ptr,
+                                        stream.cur)))
+                return st;
+            p.sample_kind = SDRGPU_C64;
+            p.in = stage_conv.ptr;
+            p.ld_in = (long)n_in;
+            st = SDRGPU_ERR_UNSUPPORTED;
+            if (want_mx() && mx_state) {
+                st = fir_mx_launch(p, mx_state, stream.cur);
+                if (st != SDRGPU_OK && st != SDRGPU_ERR_UNSUPPORTED) return st;
+            }
+        }
         if (st != SDRGPU_OK && want_os()) {
             if (!os_state && os_status == SDRGPU_OK)
-                os_state = fir_os_prepare(device, sk, tk, taps_host.data(), K, D, stream.cur,
+                os_state = fir_os_prepare(device, csk, tk, taps_host.data(), K, D, stream.cur,
                                           &os_status);
             if (os_state) st = fir_os_launch(p, os_state, stream.cur);
             if (st != SDRGPU_OK && algo == SDRGPU_FIR_OVERLAP_SAVE) return st;
@@ -189,18 +212,18 @@ struct FirCore {
         if (!in || (n_out && !out)) return SDRGPU_ERR_INVALID;
         DeviceGuard g(device);
         if (!g.ok()) return SDRGPU_ERR_DEVICE;
-        const size_t sb = sbytes();
+        const size_t ib = in_bytes(), ob = out_bytes();
         int st;
         // Stage densely (leading dimension = n_in / n_out on the device).
-        if ((st = stage_in.ensure(nch * n_in * sb))) return st;
-        if ((st = stage_out.ensure(nch * (n_out ? n_out : 1) * sb))) return st;
-        SDRGPU_HIP_TRY(hipMemcpy2DAsync(stage_in.ptr, n_in * sb, in, ld_in * sb, n_in * sb, nch,
+        if ((st = stage_in.ensure(nch * n_in * ib))) return st;
+        if ((st = stage_out.ensure(nch * (n_out ? n_out : 1) * ob))) return st;
+        SDRGPU_HIP_TRY(hipMemcpy2DAsync(stage_in.ptr, n_in * ib, in, ld_in * ib, n_in * ib, nch,
                                         hipMemcpyHostToDevice, stream.cur));
         size_t got = 0;
         if ((st = run_dev(stage_in.ptr, n_in, n_in, stage_out.ptr, n_out, &got))) return st;
         if (n_out)
-            SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * sb, stage_out.ptr, n_out * sb,
-                                            n_out * sb, nch, hipMemcpyDeviceToHost, stream.cur));
+            SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * ob, stage_out.ptr, n_out * ob,
+                                            n_out * ob, nch, hipMemcpyDeviceToHost, stream.cur));
         SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
         return SDRGPU_OK;
     }
@@ -250,10 +273,10 @@ int sdrgpu_fir_create(int device, int sample_kind, int tap_kind, const void* tap
 int sdrgpu_fir_set_algorithm(sdrgpu_fir* h, int algo) {
     if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_MATRIX) return SDRGPU_ERR_INVALID;
     if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
-        !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        !fir_os_supported(h->core.csk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     if (algo == SDRGPU_FIR_MATRIX &&
-        !fir_mx_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        !fir_mx_supported(h->core.csk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     h->core.algo = algo;
     return SDRGPU_OK;
@@ -347,10 +370,10 @@ int sdrgpu_firbank_create(int device, int sample_kind, int tap_kind, const void*
 int sdrgpu_firbank_set_algorithm(sdrgpu_firbank* h, int algo) {
     if (!h || algo < SDRGPU_FIR_AUTO || algo > SDRGPU_FIR_MATRIX) return SDRGPU_ERR_INVALID;
     if (algo == SDRGPU_FIR_OVERLAP_SAVE &&
-        !fir_os_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        !fir_os_supported(h->core.csk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     if (algo == SDRGPU_FIR_MATRIX &&
-        !fir_mx_supported(h->core.sk, h->core.tk, h->core.K, h->core.D))
+        !fir_mx_supported(h->core.csk, h->core.tk, h->core.K, h->core.D))
         return SDRGPU_ERR_UNSUPPORTED;
     h->core.algo = algo;
     return SDRGPU_OK;

@@ -351,6 +351,10 @@ void fir_mx_release(void* state) {
 
 int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     auto* st = static_cast<MxState*>(state);
+    if (st && fp.sample_kind == SDRGPU_CU8) {  // rtl_tcp u8 ingest fused into the fp16 kernel
+        if (fp.D != st->D || fp.K != st->K || !fir_mxh_supported(fp)) return SDRGPU_ERR_UNSUPPORTED;
+        return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
+    }
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
         fp.K != st->K)
         return SDRGPU_ERR_UNSUPPORTED;

@@ -61,6 +61,7 @@ struct GeoH {
 
 struct MxhParams {
     const float2* in;
+    const unsigned* in_u8;  // U8: interleaved u8 I/Q, one dword = two samples
     long ld_in, n_in;
     const float2* hist;
     float2* hist_next;
@@ -117,6 +118,38 @@ __device__ __forceinline__ float4 fetch_pair(const float2* in, const float2* his
     return make_float4(a.x, a.y, b.x, b.y);
 }
 
+// RtlTcpSignal::next (reference src/rtltcp.rs:156-164): (v - 128) / 128, exact in f32
+__device__ __forceinline__ float2 u8_iq(unsigned short w) {
+    return make_float2(((float)(w & 0xffu) - 128.0f) / 128.0f, ((float)(w >> 8) - 128.0f) / 128.0f);
+}
+// back to the u8 code of an exactly-converted sample (history written by this handle)
+__device__ __forceinline__ unsigned iq_u8(float2 v) {
+    return (unsigned)(v.x * 128.0f + 128.0f) | ((unsigned)(v.y * 128.0f + 128.0f) << 8);
+}
+// samples (j, j+1) as one dword of u8 codes, with history / zero (code 128) fill
+__device__ __forceinline__ unsigned fetch_pair_u8(const unsigned short* in, const float2* hist,
+                                                  long j, long n_in, int K) {
+    unsigned w = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const long q = j + e;
+        const bool inb = (q >= 0) & (q < n_in);
+        const bool inh = (q < 0) & (q >= -(long)(K - 1));
+        const unsigned a = in[inb ? q : 0];
+        const unsigned b = iq_u8(hist[inh ? q + (K - 1) : 0]);
+        w |= (inb ? a : (inh ? b : 0x8080u)) << (16 * e);
+    }
+    return w;
+}
+// u8 samples are integers after the x128 scale: exact in fp16, no lo planes
+template <int PLB>
+__device__ __forceinline__ void put_pair_u8(char* lds, int a, unsigned w) {
+    const float r0 = (float)(w & 0xffu) - 128.f, i0 = (float)((w >> 8) & 0xffu) - 128.f;
+    const float r1 = (float)((w >> 16) & 0xffu) - 128.f, i1 = (float)(w >> 24) - 128.f;
+    *reinterpret_cast<unsigned*>(lds + a) = pk_rtz(r0, r1);
+    *reinterpret_cast<unsigned*>(lds + a + 2 * PLB) = pk_rtz(i0, i1);
+}
+
 __device__ __forceinline__ void st32(char* lds, int a, unsigned v) {
     *reinterpret_cast<unsigned*>(lds + a) = v;
 }
@@ -151,9 +184,13 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // ABL (debug ablation, results invalid): 1 = memory only (no LDS reads / MFMA),
 // 2 = no HBM loads (compute only)
 // NT: bit 0 = non-temporal sample loads, bit 1 = non-temporal output stores
-template <int NCH, int ABL = 0, int NT = 0>
+// U8: interleaved u8 I/Q input (rtl_tcp ingest fused into the load, 2 B per sample); the
+// samples are exact integers after a fixed x128 scale, so no per-tile scale, no lo planes,
+// 2 MFMAs per component per chunk.
+template <int NCH, int ABL = 0, int NT = 0, bool U8 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
+    using Raw = std::conditional_t<U8, unsigned, float4>;
     using G = GeoH<NCH>;
     constexpr int H = G::H, PLB = G::PLB, WINB = G::WINB, NH = G::NH, KH = G::KH;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -208,71 +245,95 @@ void fir_mxh_kernel(MxhParams p) {
         const long nt = std::min(p.seg_tiles, p.tpc - t0);
         if (nt <= 0) continue;
         const float2* __restrict__ in = p.in + ch * p.ld_in;
+        const unsigned* __restrict__ in4 = p.in_u8 + ch * (p.ld_in / 2);  // U8: dword = 2 samples
+        const unsigned short* __restrict__ in2 =
+            reinterpret_cast<const unsigned short*>(p.in_u8) + ch * p.ld_in;
         const float2* __restrict__ hist = p.hist + ch * (long)(K - 1);
         float2* __restrict__ out = p.out + ch * p.ld_out;
         const long n_in = p.n_in;
         const long N0 = (long)kTileIn * t0;
         long ntf = (n_in - N0) / kTileIn;
         ntf = n_in < N0 ? 0 : (ntf > nt ? nt : ntf);
-
-        auto ldx = [&](const float2* q) {
-            const f32x4* q4 = reinterpret_cast<const f32x4*>(q);
-            const f32x4 r = (NT & 1) ? __builtin_nontemporal_load(q4) : *q4;
-            return make_float4(r[0], r[1], r[2], r[3]);
+        auto fetch = [&](long j) -> Raw {
+            if constexpr (U8) return fetch_pair_u8(in2, hist, j, n_in, K);
+            else return fetch_pair(in, hist, j, n_in, K);
         };
-        auto load_tile = [&](float4 (&dst)[8], long t) {
+        auto put = [&](int a, const Raw& w, float sc) {
+            if constexpr (U8) put_pair_u8<PLB>(smem, a, w);
+            else put_pair<PLB>(smem, a, w, sc);
+        };
+
+        // 16 B (c64 pair) or 4 B (u8 pair) per lane; j = first sample of the pair
+        auto ldx = [&](long j) -> Raw {
+            if constexpr (U8) {
+                const unsigned* q = in4 + (j >> 1);
+                return (NT & 1) ? __builtin_nontemporal_load(q) : *q;
+            } else {
+                const f32x4* q4 = reinterpret_cast<const f32x4*>(in + j);
+                const f32x4 r = (NT & 1) ? __builtin_nontemporal_load(q4) : *q4;
+                return make_float4(r[0], r[1], r[2], r[3]);
+            }
+        };
+        auto load_tile = [&](Raw (&dst)[8], long t) {
             const long j0 = N0 + (long)kTileIn * t;
             if (ABL == 2) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    dst[k] = make_float4((float)(j0 + k), 1.f, 2.f, (float)lane);
+                for (int k = 0; k < 8; ++k) {
+                    if constexpr (U8) dst[k] = (unsigned)(j0 + k + lane);
+                    else dst[k] = make_float4((float)(j0 + k), 1.f, 2.f, (float)lane);
+                }
                 return;
             }
             if (t < ntf) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    dst[k] = ldx(in + j0 + 128 * k + 2 * lane);
+                for (int k = 0; k < 8; ++k) dst[k] = ldx(j0 + 128 * k + 2 * lane);
             } else {
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    dst[k] = fetch_pair(in, hist, j0 + 128 * k + 2 * lane, n_in, K);
+                for (int k = 0; k < 8; ++k) dst[k] = fetch(j0 + 128 * k + 2 * lane);
             }
         };
-        auto window_scale = [&](const float4 (&nx)[8], const float4 (&hr)[NH]) {
-            float m = 0.f;
+        auto window_scale = [&](const Raw (&nx)[8], const Raw (&hr)[NH]) -> int {
+            if constexpr (U8) {
+                return 7;  // x128: the u8 codes minus 128, exact
+            } else {
+                float m = 0.f;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) m = absmax4(m, nx[k]);
+                for (int k = 0; k < 8; ++k) m = absmax4(m, nx[k]);
 #pragma unroll
-            for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
-            return wave_scale(m);
+                for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
+                return wave_scale(m);
+            }
         };
         auto hist_addr = [&](int k) { return (wb0 ^ (16 * (k & 7))) + 256 * k; };
         auto new_addr = [&](int k) {
             return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
         };
 
-        float4 ra[8], hr[NH];  // one raw tile in flight per wave (two waves per SIMD)
+        Raw ra[8], hr[NH];  // one raw tile in flight per wave (two waves per SIMD)
 #pragma unroll
-        for (int k = 0; k < NH; ++k)
-            hr[k] = fetch_pair(in, hist, N0 - H + 128 * k + 2 * lane, n_in, K);
+        for (int k = 0; k < NH; ++k) hr[k] = fetch(N0 - H + 128 * k + 2 * lane);
         load_tile(ra, 0);
         int s_cur = window_scale(ra, hr);
         {
             const float sc = exp2i(s_cur);
 #pragma unroll
-            for (int k = 0; k < NH; ++k) put_pair<PLB>(smem, hist_addr(k), hr[k], sc);
+            for (int k = 0; k < NH; ++k) put(hist_addr(k), hr[k], sc);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) put_pair<PLB>(smem, new_addr(k), ra[k], sc);
+            for (int k = 0; k < 8; ++k) put(new_addr(k), ra[k], sc);
 #pragma unroll
             for (int k = 0; k < NH; ++k) hr[k] = ra[KH + k];
         }
         if (nt > 1) load_tile(ra, 1);
 
-        auto body = [&](auto tau_c, long t, float4 (&nx)[8]) {
+        auto body = [&](auto tau_c, long t, Raw (&nx)[8]) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
             const bool fast2 = t + 2 < ntf;
-            const float2* src2 = fast2 ? in + N0 + (long)kTileIn * (t + 2) : p.dummy;
+            // prefetch source: the next-next tile, or the zeroed dummy buffer (scalar select)
+            const long j2 = N0 + (long)kTileIn * (t + 2);
+            const float2* src2 = fast2 ? in + j2 : p.dummy;
+            const unsigned* src2u =
+                fast2 ? in4 + (j2 >> 1) : reinterpret_cast<const unsigned*>(p.dummy);
             const int s_next = window_scale(nx, hr);
             const float scn = exp2i(s_next);
             f32x4 cr = {0.f, 0.f, 0.f, 0.f}, ci = {0.f, 0.f, 0.f, 0.f};
@@ -281,7 +342,8 @@ void fir_mxh_kernel(MxhParams p) {
                 const int a = rb[c] + TAU * WINB;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
+                    if (!U8 || (q & 1) == 0)
+                        f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
             };
             if (ABL != 1) read_frags(fb[0], 0);
 #pragma unroll
@@ -292,23 +354,32 @@ void fir_mxh_kernel(MxhParams p) {
                     const u32x4(&f)[4] = fb[c & 1];
                     cr = mfma(al[c], f[0], cr);
                     ci = mfma(al[c], f[2], ci);
-                    cr = mfma(ah[c], f[1], cr);
-                    ci = mfma(ah[c], f[3], ci);
+                    if (!U8) {
+                        cr = mfma(ah[c], f[1], cr);
+                        ci = mfma(ah[c], f[3], ci);
+                    }
                     cr = mfma(ah[c], f[0], cr);
                     ci = mfma(ah[c], f[2], ci);
                 }
                 if (c == 0) {  // next window's history = this tile's tail (old hr)
 #pragma unroll
-                    for (int k = 0; k < NH; ++k)
-                        put_pair<PLB>(smem, WN + hist_addr(k), hr[k], scn);
+                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     if ((k < NCH - 1 ? k : NCH - 1) != c) continue;
-                    put_pair<PLB>(smem, WN + new_addr(k), nx[k], scn);
+                    put(WN + new_addr(k), nx[k], scn);
                     if (k >= KH) hr[k - KH] = nx[k];
-                    if (ABL != 2)
-                        nx[k] = ldx(src2 + 128 * k + 2 * lane);
+                    if (ABL != 2) {
+                        if constexpr (U8) {
+                            const unsigned* q = src2u + 64 * k + lane;
+                            nx[k] = (NT & 1) ? __builtin_nontemporal_load(q) : *q;
+                        } else {
+                            const f32x4* q = reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane);
+                            const f32x4 r = (NT & 1) ? __builtin_nontemporal_load(q) : *q;
+                            nx[k] = make_float4(r[0], r[1], r[2], r[3]);
+                        }
+                    }
                 }
             }
             if (!fast2 && t + 2 < nt) load_tile(nx, t + 2);
@@ -353,7 +424,12 @@ void fir_mxh_kernel(MxhParams p) {
             const float2* inc = p.in + ch * p.ld_in;
             const float2* hic = p.hist + ch * (long)(K - 1);
             const long gidx = p.n_in - (long)(K - 1) + jj;
-            p.hist_next[j] = gidx >= 0 ? inc[gidx] : hic[gidx + (K - 1)];
+            if constexpr (U8) {
+                const unsigned short* inb = reinterpret_cast<const unsigned short*>(p.in_u8) + ch * p.ld_in;
+                p.hist_next[j] = gidx >= 0 ? u8_iq(inb[gidx]) : hic[gidx + (K - 1)];
+            } else {
+                p.hist_next[j] = gidx >= 0 ? inc[gidx] : hic[gidx + (K - 1)];
+            }
         }
     }
 }
@@ -368,10 +444,13 @@ int mxh_nch(int K) {
 }  // namespace
 
 int fir_mxh_supported(const FirParams& fp) {
-    if (fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != kD) return 0;
+    const bool u8 = fp.sample_kind == SDRGPU_CU8;
+    if ((!u8 && fp.sample_kind != SDRGPU_C64) || fp.tap_kind != SDRGPU_F32 || fp.D != kD) return 0;
     if (fp.K < 1 || mxh_nch(fp.K) == 0) return 0;
     if (fp.i0 < 0 || fp.i0 >= kD) return 0;
-    if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
+    // 16-byte (c64) / 4-byte (u8) loads of sample pairs: channel bases stay aligned
+    const uintptr_t align = u8 ? 3 : 15;
+    if ((reinterpret_cast<uintptr_t>(fp.in) & align) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
         return 0;
     return 1;
 }
@@ -381,7 +460,9 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     if (!fir_mxh_supported(fp) || !d_dummy) return SDRGPU_ERR_UNSUPPORTED;
     const int NCH = mxh_nch(fp.K);
     MxhParams p;
+    const bool u8 = fp.sample_kind == SDRGPU_CU8;
     p.in = static_cast<const float2*>(fp.in);
+    p.in_u8 = static_cast<const unsigned*>(fp.in);
     p.ld_in = fp.ld_in;
     p.n_in = fp.n_in;
     p.hist = static_cast<const float2*>(fp.hist);
@@ -423,7 +504,9 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                        (size_t)kWaves * GeoH<CC>::WAVE, s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (NCH == CC) {                                                                           \
-        if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0);                                                 \
+        if (u8) hipLaunchKernelGGL((fir_mxh_kernel<CC, 0, 3, true>), dim3(blocks), dim3(kBlock), \
+                                   (size_t)kWaves * GeoH<CC>::WAVE, s, p);                     \
+        else if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0);                                            \
         else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 0);                                            \
         else if (nt == 1) SDRGPU_MXH_GO(CC, 0, 1);                                             \
         else if (nt == 2) SDRGPU_MXH_GO(CC, 0, 2);                                             \

@@ -6,9 +6,9 @@ All compute runs in libsdrgpu.so (hand-written HIP for gfx950); importing this p
 without the built library raises ImportError.
 """
 from . import _lib
-from ._lib import C64, F32, SdrGpuError, device_count, lib
+from ._lib import C64, CU8, F32, SdrGpuError, device_count, lib
 from . import device, fft, filter, shard, signal  # noqa: F401
 
 lib()  # fail loudly at import if the HIP library is missing
 
-__all__ = ["device", "fft", "filter", "shard", "signal", "C64", "F32", "SdrGpuError", "device_count", "lib"]
+__all__ = ["device", "fft", "filter", "shard", "signal", "C64", "CU8", "F32", "SdrGpuError", "device_count", "lib"]

@@ -23,6 +23,7 @@ ERR_LAUNCH = 7
 
 F32 = 0
 C64 = 1
+CU8 = 2   # FIR input: interleaved u8 I/Q from rtl_tcp, (v-128)/128 fused into the load
 
 FIR_AUTO = 0
 FIR_DIRECT = 1

@@ -24,7 +24,7 @@ from typing import Optional, Sequence, Union
 import numpy as np
 
 from . import _lib
-from ._lib import C64, F32, check, lib
+from ._lib import C64, CU8, F32, check, lib
 
 
 def _kind_of(arr: np.ndarray) -> int:
@@ -36,11 +36,23 @@ def _kind_of(arr: np.ndarray) -> int:
 def _as_c(arr, kind: int) -> np.ndarray:
     if kind == C64:
         return np.ascontiguousarray(arr, dtype=np.complex64)
+    if kind == CU8:
+        # rtl_tcp byte stream: interleaved I/Q bytes, (..., 2n) or (..., n, 2)
+        return np.ascontiguousarray(arr, dtype=np.uint8)
     return np.ascontiguousarray(arr, dtype=np.float32)
 
 
+def _nsamp(x: np.ndarray, kind: int) -> int:
+    """samples along the last stream axis (CU8: 2 bytes per sample)."""
+    if kind != CU8:
+        return x.shape[-1] if x.ndim else 1
+    if x.ndim >= 2 and x.shape[-1] == 2:
+        return x.shape[-2]
+    return x.shape[-1] // 2
+
+
 def _np_dtype(kind: int):
-    return np.complex64 if kind == C64 else np.float32
+    return np.complex64 if kind in (C64, CU8) else np.float32
 
 
 # ------------------------------------------------------------------------------ FIR
@@ -139,10 +151,11 @@ class FirFilter:
     def process(self, x) -> np.ndarray:
         """Filter one block of host samples; returns the (kept) outputs."""
         x = _as_c(x, self.sample_kind)
-        n_out = self.output_len(x.size)
+        n_in = _nsamp(x.reshape(-1), self.sample_kind)
+        n_out = self.output_len(n_in)
         out = np.empty(max(n_out, 1), dtype=_np_dtype(self.sample_kind))
         got = ctypes.c_size_t()
-        check(lib().sdrgpu_fir_process(self._h, x.ctypes.data, x.size, out.ctypes.data,
+        check(lib().sdrgpu_fir_process(self._h, x.ctypes.data, n_in, out.ctypes.data,
                                        out.size, ctypes.byref(got)), "sdrgpu_fir_process")
         return out[:got.value]
 
@@ -225,9 +238,11 @@ class FirBank:
     def process(self, x) -> np.ndarray:
         """x: (nch, n) host array -> (nch, n_out)."""
         x = _as_c(x, self.sample_kind)
+        if x.ndim == 3 and self.sample_kind == CU8:
+            x = x.reshape(x.shape[0], -1)
         if x.ndim != 2 or x.shape[0] != self.nch:
             raise _lib.SdrGpuError(_lib.ERR_INVALID, "FirBank.process: shape must be (nch, n)")
-        n_in = x.shape[1]
+        n_in = _nsamp(x, self.sample_kind)
         n_out = self.output_len(n_in)
         out = np.empty((self.nch, max(n_out, 1)), dtype=_np_dtype(self.sample_kind))
         got = ctypes.c_size_t()
