@@ -236,6 +236,29 @@ int sdrgpu_pll_reset(sdrgpu_pll* h);
 int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out);
 void sdrgpu_pll_destroy(sdrgpu_pll* h);
 
+/* Batched biquad: nch independent Biquad<C, f32> filters (C = F32 or C64) designed by
+ * BiquadD::design(rate) (src/filter/biquad.rs:73-155; SDRGPU_BQ_IDENTITY = filter::Identity,
+ * src/filter/simple.rs:3-19), applied as Signal::filter (src/signal/mod.rs:42-48) with
+ * Biquad::apply's DF1 recurrence in the reference's f32 operation order (biquad.rs:42-56):
+ * outputs are bit-identical to the reference.  Channel c at in + c*ld_in samples.  The
+ * de-emphasis stage of the FM receiver (BiquadD::Lr, src/main.rs:52,75-81) is one of these. */
+typedef struct sdrgpu_biquad sdrgpu_biquad;
+
+int sdrgpu_biquad_create(int device, int sample_kind, const sdrgpu_biquad_design* d, float rate,
+                         size_t nch, sdrgpu_biquad** out);
+/* b0 b1 b2 na1 na2 as Biquad::new normalises them (biquad.rs:25-38) */
+int sdrgpu_biquad_coefs(const sdrgpu_biquad* h, float* coefs5);
+int sdrgpu_biquad_set_stream(sdrgpu_biquad* h, void* hip_stream);
+int sdrgpu_biquad_get_stream(const sdrgpu_biquad* h, void** hip_stream);
+int sdrgpu_biquad_process(sdrgpu_biquad* h, const void* in, size_t ld_in, size_t n, void* out,
+                          size_t ld_out);
+int sdrgpu_biquad_process_dev(sdrgpu_biquad* h, const void* d_in, size_t ld_in, size_t n,
+                              void* d_out, size_t ld_out);
+int sdrgpu_biquad_sync(sdrgpu_biquad* h);
+int sdrgpu_biquad_reset(sdrgpu_biquad* h);
+int sdrgpu_biquad_clone(const sdrgpu_biquad* h, sdrgpu_biquad** out);
+void sdrgpu_biquad_destroy(sdrgpu_biquad* h);
+
 /* =====================================================================================
  * Multi-GPU channel sharding (configs[4]: channels sharded across the GPUs of one node).
  * No reference counterpart (the reference is single-process CPU code):

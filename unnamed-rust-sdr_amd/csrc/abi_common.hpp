@@ -68,6 +68,9 @@ struct StreamSlot {
     }
 };
 
+// BiquadD::design -> Biquad::new coefficients b0 b1 b2 na1 na2 (abi_pll.cpp)
+int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident);
+
 inline size_t kind_bytes(int kind) { return kind == SDRGPU_C64 ? 8 : (kind == SDRGPU_CU8 ? 2 : 4); }
 
 }  // namespace detail

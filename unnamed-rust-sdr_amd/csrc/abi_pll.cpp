@@ -21,8 +21,11 @@ void bq_new(float a0, float a1, float a2, float b0, float b1, float b2, float* c
     c[4] = -a2 / a0;
 }
 
-// BiquadD::design (biquad.rs:83-155), host f32 math (glibc libm like Rust std).
-int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident) {
+}  // namespace
+
+// BiquadD::design (biquad.rs:83-155), host f32 math (glibc libm like Rust std); shared with
+// the standalone biquad ABI (abi_biquad.cpp).  This file is built with -ffp-contract=off.
+int sdrgpu::detail::bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident) {
     const float PI = 3.14159265358979323846f;
     *ident = 0;
     float omega, cs, alpha;
@@ -57,7 +60,6 @@ int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident) {
     }
 }
 
-}  // namespace
 
 struct sdrgpu_pll {
     int device = 0;

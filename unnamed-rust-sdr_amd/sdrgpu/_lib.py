@@ -141,6 +141,17 @@ SIGNATURES = [
     ("sdrgpu_pll_reset", c_int, [_H]),
     ("sdrgpu_pll_clone", c_int, [_H, _PH]),
     ("sdrgpu_pll_destroy", None, [_H]),
+    # batched biquad
+    ("sdrgpu_biquad_create", c_int, [c_int, c_int, POINTER(BiquadDesignC), c_float, c_size_t, _PH]),
+    ("sdrgpu_biquad_coefs", c_int, [_H, POINTER(c_float)]),
+    ("sdrgpu_biquad_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_biquad_get_stream", c_int, [_H, _PH]),
+    ("sdrgpu_biquad_process", c_int, [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t]),
+    ("sdrgpu_biquad_process_dev", c_int, [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t]),
+    ("sdrgpu_biquad_sync", c_int, [_H]),
+    ("sdrgpu_biquad_reset", c_int, [_H]),
+    ("sdrgpu_biquad_clone", c_int, [_H, _PH]),
+    ("sdrgpu_biquad_destroy", None, [_H]),
     # multi-GPU fan-out / gather (RCCL)
     ("sdrgpu_comm_unique_id", c_int, [c_void_p]),
     ("sdrgpu_comm_init", c_int, [c_int, c_int, c_int, c_void_p, _PH]),

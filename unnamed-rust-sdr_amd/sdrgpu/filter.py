@@ -294,6 +294,11 @@ class BiquadD:
     def to_c(self) -> _lib.BiquadDesignC:
         return _lib.BiquadDesignC(self.kind, self.freq, self.q)
 
+    def design(self, rate: float, sample_kind: int = F32, nch: int = 1,
+               device: int = 0) -> "Biquad":
+        """FilterDesign for BiquadD (biquad.rs:83-155): nch Biquad<C, f32> filters."""
+        return Biquad(self.to_c(), rate, sample_kind, nch, device)
+
 
 class _IdentityType:
     """filter::Identity (simple.rs:3-19)."""
@@ -304,6 +309,10 @@ class _IdentityType:
     def to_c(self) -> _lib.BiquadDesignC:
         return _lib.BiquadDesignC(_lib.BQ_IDENTITY, 0.0, 0.0)
 
+    def design(self, rate: float, sample_kind: int = F32, nch: int = 1,
+               device: int = 0) -> "Biquad":
+        return Biquad(self.to_c(), rate, sample_kind, nch, device)
+
     def __repr__(self):
         return "Identity"
 
@@ -312,6 +321,76 @@ Identity = _IdentityType()
 
 
 # ------------------------------------------------------------------------------ PLL
+class Biquad:
+    """nch independent Biquad<C, f32> (biquad.rs:4-56) on the GPU, bit-identical outputs;
+    `filter.Identity.design(...)` gives the pass-through (simple.rs:3-19)."""
+
+    def __init__(self, design_c, rate: float, sample_kind: int = F32, nch: int = 1,
+                 device: int = 0, _handle=None):
+        self.design_c, self.rate, self.sample_kind = design_c, rate, sample_kind
+        self.nch, self.device = nch, device
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib().sdrgpu_biquad_create(device, sample_kind, ctypes.byref(design_c), rate,
+                                             nch, ctypes.byref(self._h)), "sdrgpu_biquad_create")
+
+    def close(self):
+        if self._h:
+            lib().sdrgpu_biquad_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def coefs(self) -> np.ndarray:
+        c = (ctypes.c_float * 5)()
+        check(lib().sdrgpu_biquad_coefs(self._h, c), "sdrgpu_biquad_coefs")
+        return np.array(c[:], dtype=np.float32)
+
+    def clone(self) -> "Biquad":
+        h = ctypes.c_void_p()
+        check(lib().sdrgpu_biquad_clone(self._h, ctypes.byref(h)), "sdrgpu_biquad_clone")
+        return Biquad(self.design_c, self.rate, self.sample_kind, self.nch, self.device,
+                      _handle=h)
+
+    def reset(self):
+        check(lib().sdrgpu_biquad_reset(self._h), "sdrgpu_biquad_reset")
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(lib().sdrgpu_biquad_get_stream(self._h, ctypes.byref(s)), "get_stream")
+        return s.value or 0
+
+    def process(self, x) -> np.ndarray:
+        """x: (n,) for one channel or (nch, n) -> same shape, filtered."""
+        x = _as_c(x, self.sample_kind)
+        one = x.ndim == 1
+        x2 = x.reshape(1, -1) if one else x
+        if x2.shape[0] != self.nch:
+            raise _lib.SdrGpuError(_lib.ERR_INVALID, "Biquad.process: shape must be (nch, n)")
+        n = x2.shape[1]
+        out = np.empty_like(x2)
+        check(lib().sdrgpu_biquad_process(self._h, x2.ctypes.data, n, n, out.ctypes.data, n),
+              "sdrgpu_biquad_process")
+        return out[0] if one else out
+
+    def apply(self, value):
+        """Filter::apply for one sample (biquad.rs:42-56)."""
+        return self.process(np.asarray([value]))[0]
+
+    def process_dev(self, d_in, ld_in, n, d_out, ld_out):
+        check(lib().sdrgpu_biquad_process_dev(self._h, d_in, ld_in, n, d_out, ld_out),
+              "sdrgpu_biquad_process_dev")
+
+    def sync(self):
+        check(lib().sdrgpu_biquad_sync(self._h), "sdrgpu_biquad_sync")
+
+
 class PllDesign:
     """PllDesign::new(reference, gain, loopfilter, outputfilter, lockfilter)
     (pll.rs:25-37).  design(rate) -> Pll over `nch` independent channels."""
