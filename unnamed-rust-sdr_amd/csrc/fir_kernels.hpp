@@ -52,8 +52,9 @@ int fir_mxl_launch(const FirParams& p, const float* d_taps, const void* d_dummy,
                    hipStream_t s);
 
 // Same shape on a per-tile scaled two-way fp16 split, two waves per SIMD (fir_mxh.hip):
-// K <= 257.  tap_scale_exp: taps are multiplied by 2^tap_scale_exp before the split.
+// D = 4 (K <= 257, also u8 input) and D = 1 (K <= 273).  tap_scale_exp: taps are multiplied by 2^tap_scale_exp before the split.
 int fir_mxh_supported(const FirParams& p);
+int fir_mxh_shape_ok(int sample_kind, int tap_kind, int K, int D);  // D in {1, 4}
 int fir_mxh_launch(const FirParams& p, const float* d_taps, int tap_scale_exp,
                    const void* d_dummy, int cus, hipStream_t s);
 

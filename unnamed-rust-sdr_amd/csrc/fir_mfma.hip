@@ -268,9 +268,10 @@ void fir_mx_kernel(MxParams p) {
         }
     }
 
-    if (blockIdx.x == gridDim.x - 1 && p.hist_next) {  // stream history carry
+    if (p.hist_next) {  // stream history carry, spread over the whole grid
         const long nch = (p.nseg + p.nseg_ch - 1) / p.nseg_ch;
-        for (long j = threadIdx.x; j < nch * (K - 1); j += kMxBlock) {
+        for (long j = (long)blockIdx.x * kMxBlock + threadIdx.x; j < nch * (K - 1);
+             j += (long)gridDim.x * kMxBlock) {
             const long ch = j / (K - 1), jj = j - ch * (K - 1);
             const float2* inc = p.in + ch * p.ld_in;
             const float2* hic = p.hist + ch * (long)(K - 1);
@@ -289,6 +290,7 @@ struct MxState {
 };
 
 int mx_nch(int K, int D) {
+    if (!(D == 2 || D == 4 || D == 8)) return 0;
     // smallest instantiated chunk count covering the K + 15D + 1 window
     const int need = (K + 15 * D + 1 + 31) / 32;
     static const int c2[] = {4, 9}, c4[] = {4, 10}, c8[] = {4, 12};
@@ -302,6 +304,7 @@ int mx_nch(int K, int D) {
 }  // namespace
 
 int fir_mx_supported(int sample_kind, int tap_kind, int K, int D) {
+    if (fir_mxh_shape_ok(sample_kind, tap_kind, K, D)) return 1;
     if (sample_kind != SDRGPU_C64 || tap_kind != SDRGPU_F32) return 0;
     if (!(D == 2 || D == 4 || D == 8) || K < 1) return 0;
     return mx_nch(K, D) > 0;
@@ -369,6 +372,7 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
     if (variant >= 2 && fir_mxl_supported(fp))
         return fir_mxl_launch(fp, st->d_taps, st->d_dummy, st->cus, s);
+    if (st->NCH == 0) return SDRGPU_ERR_UNSUPPORTED;  // shape only the fp16 kernel covers
     // 16-byte loads of sample pairs: channel bases must stay 16-byte aligned
     if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
         return SDRGPU_ERR_UNSUPPORTED;

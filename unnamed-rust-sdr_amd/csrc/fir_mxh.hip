@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "fir_kernels.hpp"
 
@@ -40,22 +41,23 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kD = 4;
 constexpr int kTileOut = 256;
-constexpr int kTileIn = kTileOut * kD;  // 1024 new samples per tile
 constexpr int kWaves = 8;               // two waves per SIMD
 constexpr int kBlock = 64 * kWaves;
 
-template <int NCH>
+template <int NCH, int D = 4>
 struct GeoH {
-    static constexpr int H = 32 * NCH - 16 * kD;  // history samples of a tile's window
-    static constexpr int WL = H + kTileIn;        // window samples
-    static constexpr int PLB = 2 * WL;            // bytes per plane
-    static constexpr int WINB = 4 * PLB;          // bytes per window buffer
-    static constexpr int WAVE = 2 * WINB;         // bytes per wave
-    static constexpr int NH = H / 128;            // history groups
-    static constexpr int KH = 8 - NH;             // first tile group that is next history
-    static_assert(H % 128 == 0 && H > 0 && H < kTileIn, "geometry");
+    static constexpr int TI = 256 * D;             // new samples per tile (256 outputs)
+    static constexpr int HR = 32 * NCH - 16 * D;   // history samples a tile's windows need
+    static constexpr int H = (HR + 127) / 128 * 128;  // staged history (128-sample groups)
+    static constexpr int OFF = H - HR;             // window offset inside the buffer
+    static constexpr int WL = H + TI;              // window samples
+    static constexpr int PLB = 2 * WL;             // bytes per plane
+    static constexpr int WINB = 4 * PLB;           // bytes per window buffer
+    static constexpr int WAVE = 2 * WINB;          // bytes per wave
+    static constexpr int NG = TI / 128;            // 128-sample groups per tile
+    static constexpr int NH = H / 128;             // history groups
+    static_assert(HR > 0 && (D == 1 || (D == 4 && OFF == 0)), "geometry");
     static_assert(kWaves * WAVE <= 160 * 1024, "LDS");
 };
 
@@ -170,13 +172,25 @@ __device__ __forceinline__ float absmax4(float m, const float4& f) {
     return fmaxf(fmaxf(m, fmaxf(fabsf(f.x), fabsf(f.y))), fmaxf(fabsf(f.z), fabsf(f.w)));
 }
 
-// window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float
+// window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float.  The
+// wave max uses DPP row reductions + 4 readlanes (non-negative floats order like their
+// bits): no LDS round trips on the per-tile critical path.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_umax(unsigned x) {
+    const unsigned y = (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false);
+    return x > y ? x : y;
+}
 __device__ __forceinline__ int wave_scale(float m) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    int s = 15 - __builtin_amdgcn_frexp_expf(m);
-    s = s < -126 ? -126 : (s > 126 ? 126 : s);
-    return __builtin_amdgcn_readfirstlane(s);
+    unsigned x = __float_as_uint(m);
+    x = dpp_umax<0xB1>(x);   // quad_perm [1,0,3,2]
+    x = dpp_umax<0x4E>(x);   // quad_perm [2,3,0,1]
+    x = dpp_umax<0x141>(x);  // row_half_mirror
+    x = dpp_umax<0x140>(x);  // row_mirror: every lane holds its row's max
+    const unsigned a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+    const unsigned c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
+    const unsigned ab = a > b ? a : b, cd = c > d ? c : d;
+    int s = 15 - __builtin_amdgcn_frexp_expf(__uint_as_float(ab > cd ? ab : cd));
+    return s < -126 ? -126 : (s > 126 ? 126 : s);
 }
 
 __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1.0f, s); }
@@ -187,12 +201,15 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // U8: interleaved u8 I/Q input (rtl_tcp ingest fused into the load, 2 B per sample); the
 // samples are exact integers after a fixed x128 scale, so no per-tile scale, no lo planes,
 // 2 MFMAs per component per chunk.
-template <int NCH, int ABL = 0, int NT = 0, bool U8 = false>
+// D: decimation 4 (XOR-swizzled LDS rows, block map sigma) or 1 (linear LDS: blocks 16
+// samples apart already hit distinct banks; identity block map).
+template <int NCH, int ABL = 0, int NT = 0, bool U8 = false, int D = 4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
-    using G = GeoH<NCH>;
-    constexpr int H = G::H, PLB = G::PLB, WINB = G::WINB, NH = G::NH, KH = G::KH;
+    using G = GeoH<NCH, D>;
+    constexpr int H = G::H, HR = G::HR, PLB = G::PLB, WINB = G::WINB, NH = G::NH, NG = G::NG;
+    constexpr int TI = G::TI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int lane = threadIdx.x & 63;
@@ -215,7 +232,7 @@ void fir_mxh_kernel(MxhParams p) {
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int pidx = 32 * c + 8 * g + 2 * jj + e;
-                    const int k = 4 * v + 3 - p.delta + H - pidx;
+                    const int k = D * v + D - 1 - p.delta + HR - pidx;
                     const bool ok = (k >= 0) & (k < K);
                     const float hk = p.taps[ok ? k : 0];
                     const float hs = ok ? hk * tsc : 0.f;
@@ -230,14 +247,19 @@ void fir_mxh_kernel(MxhParams p) {
         }
     }
 
-    const int sv = sigma(v);
+    const int sv = D == 4 ? sigma(v) : v;
     int rb[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        const int r = sv + (c >> 1);
-        rb[c] = base + 128 * r + 16 * ((4 * (c & 1) + g) ^ ((r >> 1) & 7));
+        if constexpr (D == 4) {
+            const int r = sv + (c >> 1);
+            rb[c] = base + 128 * r + 16 * ((4 * (c & 1) + g) ^ ((r >> 1) & 7));
+        } else {
+            rb[c] = base + 2 * (G::OFF + 16 * sv + 32 * c + 8 * g);
+        }
     }
-    const int wb0 = base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7);
+    const int wb0 = D == 4 ? base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7)
+                           : base + 4 * lane;
 
     for (long u = wave; u < p.units; u += nwaves) {
         const long ch = u / p.spc;
@@ -251,8 +273,8 @@ void fir_mxh_kernel(MxhParams p) {
         const float2* __restrict__ hist = p.hist + ch * (long)(K - 1);
         float2* __restrict__ out = p.out + ch * p.ld_out;
         const long n_in = p.n_in;
-        const long N0 = (long)kTileIn * t0;
-        long ntf = (n_in - N0) / kTileIn;
+        const long N0 = (long)TI * t0;
+        long ntf = (n_in - N0) / TI;
         ntf = n_in < N0 ? 0 : (ntf > nt ? nt : ntf);
         auto fetch = [&](long j) -> Raw {
             if constexpr (U8) return fetch_pair_u8(in2, hist, j, n_in, K);
@@ -274,11 +296,11 @@ void fir_mxh_kernel(MxhParams p) {
                 return make_float4(r[0], r[1], r[2], r[3]);
             }
         };
-        auto load_tile = [&](Raw (&dst)[8], long t) {
-            const long j0 = N0 + (long)kTileIn * t;
+        auto load_tile = [&](Raw (&dst)[NG], long t) {
+            const long j0 = N0 + (long)TI * t;
             if (ABL == 2) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
+                for (int k = 0; k < NG; ++k) {
                     if constexpr (U8) dst[k] = (unsigned)(j0 + k + lane);
                     else dst[k] = make_float4((float)(j0 + k), 1.f, 2.f, (float)lane);
                 }
@@ -286,56 +308,80 @@ void fir_mxh_kernel(MxhParams p) {
             }
             if (t < ntf) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) dst[k] = ldx(j0 + 128 * k + 2 * lane);
+                for (int k = 0; k < NG; ++k) dst[k] = ldx(j0 + 128 * k + 2 * lane);
             } else {
+                // stream start / end only: keep this path out of the hot loop (the clamped,
+                // always-dereferenceable loads would otherwise be speculated into every tile)
+                asm volatile("" ::: "memory");
 #pragma unroll
-                for (int k = 0; k < 8; ++k) dst[k] = fetch(j0 + 128 * k + 2 * lane);
+                for (int k = 0; k < NG; ++k) dst[k] = fetch(j0 + 128 * k + 2 * lane);
             }
         };
-        auto window_scale = [&](const Raw (&nx)[8], const Raw (&hr)[NH]) -> int {
+        auto window_scale = [&](const Raw (&nx)[NG], const Raw (&hr)[NH]) -> int {
             if constexpr (U8) {
                 return 7;  // x128: the u8 codes minus 128, exact
             } else {
                 float m = 0.f;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) m = absmax4(m, nx[k]);
+                for (int k = 0; k < NG; ++k) m = absmax4(m, nx[k]);
 #pragma unroll
                 for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
                 return wave_scale(m);
             }
         };
-        auto hist_addr = [&](int k) { return (wb0 ^ (16 * (k & 7))) + 256 * k; };
+        // byte offset of the sample pair (2 lane, 2 lane + 1) of history group k / new group k
+        auto hist_addr = [&](int k) {
+            if constexpr (D == 4) return (wb0 ^ (16 * (k & 7))) + 256 * k;
+            else return wb0 + 256 * k;
+        };
         auto new_addr = [&](int k) {
-            return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
+            if constexpr (D == 4) return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
+            else return wb0 + 2 * H + 256 * k;
+        };
+        // next history = the last NH groups of (history ++ this tile's groups)
+        auto roll_hist = [&](Raw (&hr)[NH], const Raw (&tile)[NG]) {
+            Raw nh[NH];
+#pragma unroll
+            for (int i = 0; i < NH; ++i) nh[i] = NG + i < NH ? hr[(NG + i) % NH] : tile[(NG + i - NH) % NG];
+#pragma unroll
+            for (int i = 0; i < NH; ++i) hr[i] = nh[i];
         };
 
-        Raw ra[8], hr[NH];  // one raw tile in flight per wave (two waves per SIMD)
+        // PD raw tiles in flight per wave (8 groups' worth of registers: 1 tile at D = 4,
+        // 4 at D = 1, whose tiles are 4x shorter); rr[t % PD] holds tile t until staged
+        constexpr int PD = 8 / NG;
+        Raw rr[PD][NG], hr[NH];
 #pragma unroll
         for (int k = 0; k < NH; ++k) hr[k] = fetch(N0 - H + 128 * k + 2 * lane);
-        load_tile(ra, 0);
-        int s_cur = window_scale(ra, hr);
+        load_tile(rr[0], 0);
+#pragma unroll
+        for (int q = 1; q < PD; ++q)
+            if (q < nt) load_tile(rr[q], q);
+        int s_cur = window_scale(rr[0], hr);
         {
             const float sc = exp2i(s_cur);
 #pragma unroll
             for (int k = 0; k < NH; ++k) put(hist_addr(k), hr[k], sc);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) put(new_addr(k), ra[k], sc);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) hr[k] = ra[KH + k];
+            for (int k = 0; k < NG; ++k) put(new_addr(k), rr[0][k], sc);
+            roll_hist(hr, rr[0]);
         }
-        if (nt > 1) load_tile(ra, 1);
+        if (PD < nt) load_tile(rr[0], PD);
 
-        auto body = [&](auto tau_c, long t, Raw (&nx)[8]) {
+        auto body = [&](auto tau_c, long t, Raw (&nx)[NG]) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
-            const bool fast2 = t + 2 < ntf;
-            // prefetch source: the next-next tile, or the zeroed dummy buffer (scalar select)
-            const long j2 = N0 + (long)kTileIn * (t + 2);
+            const long tp = t + 1 + PD;  // the tile whose loads replace nx's
+            const bool fast2 = tp < ntf;
+            // prefetch source: tile tp, or the zeroed dummy buffer (scalar select)
+            const long j2 = N0 + (long)TI * tp;
             const float2* src2 = fast2 ? in + j2 : p.dummy;
             const unsigned* src2u =
                 fast2 ? in4 + (j2 >> 1) : reinterpret_cast<const unsigned*>(p.dummy);
             const int s_next = window_scale(nx, hr);
             const float scn = exp2i(s_next);
+            constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
+            Raw keep[NK];
             f32x4 cr = {0.f, 0.f, 0.f, 0.f}, ci = {0.f, 0.f, 0.f, 0.f};
             u32x4 fb[2][4];
             auto read_frags = [&](u32x4 (&f)[4], int c) {
@@ -366,10 +412,10 @@ void fir_mxh_kernel(MxhParams p) {
                     for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
                 }
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
+                for (int k = 0; k < NG; ++k) {
                     if ((k < NCH - 1 ? k : NCH - 1) != c) continue;
                     put(WN + new_addr(k), nx[k], scn);
-                    if (k >= KH) hr[k - KH] = nx[k];
+                    if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
                     if (ABL != 2) {
                         if constexpr (U8) {
                             const unsigned* q = src2u + 64 * k + lane;
@@ -382,9 +428,15 @@ void fir_mxh_kernel(MxhParams p) {
                     }
                 }
             }
-            if (!fast2 && t + 2 < nt) load_tile(nx, t + 2);
+            {   // history of tile t+2's window: roll in the staged tile's tail
+                Raw tile[NG];
+#pragma unroll
+                for (int k = 0; k < NG; ++k) tile[k] = keep[k < (NG > NH ? NG - NH : 0) ? 0 : k - (NG > NH ? NG - NH : 0)];
+                roll_hist(hr, tile);
+            }
+            if (!fast2 && tp < nt) load_tile(nx, tp);
             const int so = -(s_cur + p.sh);
-            const long m = (t0 + t) * kTileOut + 16 * sv + 4 * g;
+            const long m = (t0 + t) * kTileOut + 16 * sv + 4 * g;  // sv = block of column v
             float yr[4], yi[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -410,16 +462,23 @@ void fir_mxh_kernel(MxhParams p) {
             s_cur = s_next;
         };
 
-        for (long t = 0; t < nt; t += 2) {
-            body(std::integral_constant<int, 0>(), t, ra);
-            if (t + 1 >= nt) break;
-            body(std::integral_constant<int, 1>(), t + 1, ra);
+        // unrolled over lcm(2, PD) tiles: ring half (t & 1) and raw slot ((t + 1) % PD) are
+        // compile-time in every body
+        constexpr int U = PD > 2 ? PD : 2;
+        for (long t = 0; t < nt; t += U) {
+            [&]<int... I>(std::integer_sequence<int, I...>) {
+                bool go = true;
+                ((go = go && (t + I < nt),
+                  go ? (body(std::integral_constant<int, I & 1>(), t + I, rr[(I + 1) % PD]), 0) : 0),
+                 ...);
+            }(std::make_integer_sequence<int, U>());
         }
     }
 
-    if (blockIdx.x == gridDim.x - 1 && p.hist_next) {  // stream history carry
+    if (p.hist_next) {  // stream history carry, spread over the whole grid
         const long nch = p.units / p.spc;
-        for (long j = threadIdx.x; j < nch * (K - 1); j += kBlock) {
+        for (long j = (long)blockIdx.x * kBlock + threadIdx.x; j < nch * (K - 1);
+             j += (long)gridDim.x * kBlock) {
             const long ch = j / (K - 1), jj = j - ch * (K - 1);
             const float2* inc = p.in + ch * p.ld_in;
             const float2* hic = p.hist + ch * (long)(K - 1);
@@ -434,20 +493,32 @@ void fir_mxh_kernel(MxhParams p) {
     }
 }
 
-int mxh_nch(int K) {
-    const int need = (K + 63 + 31) / 32;  // 32 NCH >= K + 15*4 + 3
-    if (need <= 6) return 6;
-    if (need <= 10) return 10;
+int mxh_nch(int K, int D) {
+    if (D == 4) {
+        const int need = (K + 63 + 31) / 32;  // 32 NCH >= K + 15*4 + 3
+        return need <= 6 ? 6 : (need <= 10 ? 10 : 0);
+    }
+    if (D == 1) {
+        const int need = (K + 15 + 31) / 32;  // 32 NCH >= K + 15
+        return need <= 5 ? 5 : (need <= 9 ? 9 : 0);
+    }
     return 0;
 }
 
 }  // namespace
 
+int fir_mxh_shape_ok(int sample_kind, int tap_kind, int K, int D) {
+    if (tap_kind != SDRGPU_F32 || K < 1) return 0;
+    if (sample_kind == SDRGPU_CU8) return D == 4 && mxh_nch(K, 4) > 0;
+    return sample_kind == SDRGPU_C64 && mxh_nch(K, D) > 0;
+}
+
 int fir_mxh_supported(const FirParams& fp) {
     const bool u8 = fp.sample_kind == SDRGPU_CU8;
-    if ((!u8 && fp.sample_kind != SDRGPU_C64) || fp.tap_kind != SDRGPU_F32 || fp.D != kD) return 0;
-    if (fp.K < 1 || mxh_nch(fp.K) == 0) return 0;
-    if (fp.i0 < 0 || fp.i0 >= kD) return 0;
+    if ((!u8 && fp.sample_kind != SDRGPU_C64) || fp.tap_kind != SDRGPU_F32) return 0;
+    if (!(fp.D == 4 || (fp.D == 1 && !u8))) return 0;
+    if (fp.K < 1 || mxh_nch(fp.K, fp.D) == 0) return 0;
+    if (fp.i0 < 0 || fp.i0 >= fp.D) return 0;
     // 16-byte (c64) / 4-byte (u8) loads of sample pairs: channel bases stay aligned
     const uintptr_t align = u8 ? 3 : 15;
     if ((reinterpret_cast<uintptr_t>(fp.in) & align) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
@@ -458,7 +529,8 @@ int fir_mxh_supported(const FirParams& fp) {
 int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                    const void* d_dummy, int cus, hipStream_t s) {
     if (!fir_mxh_supported(fp) || !d_dummy) return SDRGPU_ERR_UNSUPPORTED;
-    const int NCH = mxh_nch(fp.K);
+    const int D = fp.D;
+    const int NCH = mxh_nch(fp.K, D);
     MxhParams p;
     const bool u8 = fp.sample_kind == SDRGPU_CU8;
     p.in = static_cast<const float2*>(fp.in);
@@ -470,7 +542,7 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     p.dummy = static_cast<const float2*>(d_dummy);
     p.n_out = fp.n_out;
     p.K = fp.K;
-    p.delta = (int)(kD - 1 - fp.i0);
+    p.delta = (int)(D - 1 - fp.i0);
     p.sh = tap_scale_exp;
     p.taps = d_taps;
     p.out = static_cast<float2*>(fp.out);
@@ -499,25 +571,35 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
         const char* e = getenv("SDRGPU_MXH_NT");  // default: both non-temporal (streamed once)
         return e ? atoi(e) : 3;
     }();
-#define SDRGPU_MXH_GO(CC, A, N)                                                                 \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, A, N>), dim3(blocks), dim3(kBlock),                 \
-                       (size_t)kWaves * GeoH<CC>::WAVE, s, p)
+#define SDRGPU_MXH_GO(CC, A, N, U, DD)                                                         \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, A, N, U, DD>), dim3(blocks), dim3(kBlock),          \
+                       (size_t)kWaves * (GeoH<CC, DD>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
-    if (NCH == CC) {                                                                           \
-        if (u8) hipLaunchKernelGGL((fir_mxh_kernel<CC, 0, 3, true>), dim3(blocks), dim3(kBlock), \
-                                   (size_t)kWaves * GeoH<CC>::WAVE, s, p);                     \
-        else if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0);                                            \
-        else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 0);                                            \
-        else if (nt == 1) SDRGPU_MXH_GO(CC, 0, 1);                                             \
-        else if (nt == 2) SDRGPU_MXH_GO(CC, 0, 2);                                             \
-        else if (nt == 3) SDRGPU_MXH_GO(CC, 0, 3);                                             \
-        else SDRGPU_MXH_GO(CC, 0, 0);                                                          \
+    if (D == 4 && NCH == CC) {                                                                 \
+        if (u8) SDRGPU_MXH_GO(CC, 0, 3, true, 4);                                              \
+        else if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0, false, 4);                                  \
+        else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 0, false, 4);                                  \
+        else if (nt == 1) SDRGPU_MXH_GO(CC, 0, 1, false, 4);                                   \
+        else if (nt == 2) SDRGPU_MXH_GO(CC, 0, 2, false, 4);                                   \
+        else if (nt == 3) SDRGPU_MXH_GO(CC, 0, 3, false, 4);                                   \
+        else SDRGPU_MXH_GO(CC, 0, 0, false, 4);                                                \
+        SDRGPU_LAUNCH_CHECK();                                                                 \
+        return SDRGPU_OK;                                                                      \
+    }
+#define SDRGPU_MXH_CASE1(CC)                                                                   \
+    if (D == 1 && NCH == CC) {                                                                 \
+        if (abl == 1) SDRGPU_MXH_GO(CC, 1, 3, false, 1);                                       \
+        else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 3, false, 1);                                  \
+        else SDRGPU_MXH_GO(CC, 0, 3, false, 1);                                                \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
     SDRGPU_MXH_CASE(10)
     SDRGPU_MXH_CASE(6)
+    SDRGPU_MXH_CASE1(9)
+    SDRGPU_MXH_CASE1(5)
 #undef SDRGPU_MXH_CASE
+#undef SDRGPU_MXH_CASE1
 #undef SDRGPU_MXH_GO
     return SDRGPU_ERR_UNSUPPORTED;
 }

@@ -326,9 +326,10 @@ void fir_mxl_kernel(MxlParams p) {
         }
     }
 
-    if (blockIdx.x == gridDim.x - 1 && p.hist_next) {  // stream history carry
+    if (p.hist_next) {  // stream history carry, spread over the whole grid
         const long nch = p.units / p.spc;
-        for (long j = threadIdx.x; j < nch * (K - 1); j += kBlock) {
+        for (long j = (long)blockIdx.x * kBlock + threadIdx.x; j < nch * (K - 1);
+             j += (long)gridDim.x * kBlock) {
             const long ch = j / (K - 1), jj = j - ch * (K - 1);
             const float2* inc = p.in + ch * p.ld_in;
             const float2* hic = p.hist + ch * (long)(K - 1);
