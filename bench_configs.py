@@ -38,7 +38,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "all"])
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -142,6 +142,29 @@ def bench_c2u8(args):
                       "(v-128)/128 fused into the load, 2^28 samples",
             "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
             "roofline": roof(2 + 8 / 4, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
+
+
+# ------------------------------------------------------------------------------ c2host
+def bench_c2host(args):
+    """configs[1] through the HOST-pointer entry point (sdrgpu_fir_process: pageable numpy
+    buffers, H2D + kernel + D2H on the handle's stream): the PCIe-inclusive rate."""
+    import scipy.signal as ss
+    import sdrgpu
+    n = 1 << 26
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    fir = sdrgpu.filter.Fir(taps, decim=4, sample_kind=sdrgpu.C64).design(2.4e6)
+    x = cplx_pattern(n, 5)
+    fir.process(x)  # warm-up (staging buffers)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = fir.process(x)
+    el = (time.perf_counter() - t0) / args.steps
+    assert y.size == n // 4
+    return {"config": "c2host: configs[1] via sdrgpu_fir_process (pageable host buffers, "
+                      "H2D + FIR + D2H), 2^26 samples per call",
+            "metric": "complex Msamples/s (input, PCIe-inclusive)", "value": round(n / el / 1e6, 1),
+            "wall_ms_per_call": round(el * 1e3, 3),
+            "host_bytes_per_s": round(10 * n / el / 1e9, 2)}
 
 
 # ------------------------------------------------------------------------------ c4
@@ -263,9 +286,10 @@ def bench_c5(args):
 
 def main():
     args = parse()
-    todo = ["c3", "c4", "c5", "c2u8"] if args.config == "all" else [args.config]
+    todo = ["c3", "c4", "c5", "c2u8", "c2host"] if args.config == "all" else [args.config]
     for c in todo:
-        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8}[c](args)
+        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
+             "c2host": bench_c2host}[c](args)
         if r is not None:
             print(json.dumps(r), flush=True)
 

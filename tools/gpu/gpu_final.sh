@@ -18,4 +18,8 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $R/bench.py > $O/trace.log 2>&1 || { tail -5 $O/trace.log; exit 4; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || { tail -5 $O/pmc_fetch.log; exit 5; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1 || { tail -5 $O/pmc_write.log; exit 6; }
-echo done
+echo pmc done
+cd $R
+timeout -k 10 600 python bench_configs.py --config all > $O/configs.log 2>&1 || { tail -5 $O/configs.log; exit 7; }
+grep '^{' $O/configs.log > $O/configs.jsonl
+echo configs done
