@@ -260,6 +260,71 @@ int sdrgpu_biquad_clone(const sdrgpu_biquad* h, sdrgpu_biquad** out);
 void sdrgpu_biquad_destroy(sdrgpu_biquad* h);
 
 /* =====================================================================================
+ * Sample-rate conversion: the libsamplerate surface src/resample.rs binds through
+ * libsamplerate-sys (SampleRate::new -> src_new :32-44, process -> src_process :46-67,
+ * reset -> src_reset :72-77, try_clone -> src_clone :79-86, channels -> src_get_channels
+ * :88-92, set_ratio -> src_set_ratio :94-99, Drop -> src_delete :103-110, version
+ * :3-8, ConverterType::name/description :121-135, Error::description :189-196), so the
+ * Rust wrapper swaps `src_*` for `sdrgpu_src_*` and keeps its Error::from_c mapping
+ * (:236-262): these functions return LIBSAMPLERATE error codes (0 = ok, 1..22 as in
+ * sdrgpu_src_error below), not sdrgpu_status.
+ *
+ * Converters: SDRGPU_SRC_ZERO_ORDER_HOLD and SDRGPU_SRC_LINEAR follow libsamplerate's
+ * src_zoh.c / src_linear.c exactly (f64 position walk, f32 samples, state carried across
+ * calls).  The three sinc converters need libsamplerate's coefficient tables, which are not
+ * in this image: sdrgpu_src_new returns SRC_ERR_BAD_CONVERTER for them.
+ *
+ * Frames hold `channels` interleaved f32 (f32 = 1, Complex<f32> = 2, (A, B) = sum;
+ * src/resample.rs:272-282); a large channel count batches many independent streams that
+ * share one ratio.  sdrgpu_src_process takes HOST pointers and is synchronous;
+ * sdrgpu_src_process_dev takes DEVICE pointers, fills the frame counts at once and
+ * enqueues the conversion on the handle's stream (sdrgpu_src_sync to wait).
+ * ===================================================================================== */
+enum sdrgpu_src_converter {       /* libsamplerate's converter ids */
+    SDRGPU_SRC_SINC_BEST_QUALITY = 0,
+    SDRGPU_SRC_SINC_MEDIUM_QUALITY = 1,
+    SDRGPU_SRC_SINC_FASTEST = 2,
+    SDRGPU_SRC_ZERO_ORDER_HOLD = 3,
+    SDRGPU_SRC_LINEAR = 4,
+};
+enum sdrgpu_src_error {           /* libsamplerate's codes, as src/resample.rs:208-234 */
+    SDRGPU_SRC_ERR_MALLOC_FAILED = 1,
+    SDRGPU_SRC_ERR_BAD_STATE = 2,
+    SDRGPU_SRC_ERR_BAD_DATA = 3,
+    SDRGPU_SRC_ERR_BAD_DATA_PTR = 4,
+    SDRGPU_SRC_ERR_BAD_SRC_RATIO = 6,
+    SDRGPU_SRC_ERR_BAD_CONVERTER = 10,
+    SDRGPU_SRC_ERR_BAD_CHANNEL_COUNT = 11,
+    SDRGPU_SRC_ERR_DATA_OVERLAP = 16,
+    SDRGPU_SRC_ERR_BAD_INTERNAL_STATE = 22,
+};
+/* layout of libsamplerate's SRC_DATA (the struct SampleRate::process fills, :47-56) */
+typedef struct {
+    const float* data_in;
+    float* data_out;
+    long input_frames, output_frames;
+    long input_frames_used, output_frames_gen;
+    int end_of_input;
+    double src_ratio;             /* output rate / input rate, in [1/256, 256] */
+} sdrgpu_src_data;
+
+typedef struct sdrgpu_src_state sdrgpu_src_state;
+sdrgpu_src_state* sdrgpu_src_new(int device, int converter_type, int channels, int* error);
+int sdrgpu_src_process(sdrgpu_src_state* s, sdrgpu_src_data* data);
+int sdrgpu_src_process_dev(sdrgpu_src_state* s, sdrgpu_src_data* data);
+int sdrgpu_src_sync(sdrgpu_src_state* s);
+int sdrgpu_src_reset(sdrgpu_src_state* s);
+sdrgpu_src_state* sdrgpu_src_clone(sdrgpu_src_state* s, int* error);
+int sdrgpu_src_get_channels(sdrgpu_src_state* s);   /* negative error code on a null handle */
+int sdrgpu_src_set_ratio(sdrgpu_src_state* s, double new_ratio);
+int sdrgpu_src_set_stream(sdrgpu_src_state* s, void* hip_stream);
+sdrgpu_src_state* sdrgpu_src_delete(sdrgpu_src_state* s);  /* returns NULL, as src_delete */
+const char* sdrgpu_src_strerror(int error);
+const char* sdrgpu_src_get_name(int converter_type);        /* NULL for unknown ids */
+const char* sdrgpu_src_get_description(int converter_type);
+const char* sdrgpu_src_get_version(void);
+
+/* =====================================================================================
  * Multi-GPU channel sharding (configs[4]: channels sharded across the GPUs of one node).
  * No reference counterpart (the reference is single-process CPU code):
  * channels are independent, so the only collectives are the fan-out of channel blocks from

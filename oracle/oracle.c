@@ -463,3 +463,128 @@ void oracle_freq(float rate, float freq, float phase, size_t n, float* out) {
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
     for (size_t i = 0; i < 2 * n; ++i) out[i] = ((float)in[i] - 128.0f) / 128.0f;
 }
+
+/* ======================= sample-rate conversion (libsamplerate) =====================
+ * src/resample.rs:46-67 fills an SRC_DATA and calls src_process; restated here are
+ * samplerate.c's src_process checks and src_zoh.c / src_linear.c's process loops, counting
+ * in samples (frames x channels) as those files do. */
+struct oracle_src {
+    int converter, channels, reset;
+    double last_ratio, last_position;
+    float* last_value;
+};
+
+static double src_fmod_one(double x) {
+    double res = x - lrint(x);
+    if (res < 0.0) return res + 1.0;
+    return res;
+}
+
+static int src_bad_ratio(double r) { return r < (1.0 / 256.0) || r > 256.0; }
+
+oracle_src* oracle_src_new(int converter, int channels, int* error) {
+    *error = 0;
+    if (converter != 3 && converter != 4) { *error = 10; return NULL; }
+    if (channels < 1) { *error = 11; return NULL; }
+    oracle_src* s = (oracle_src*)calloc(1, sizeof(*s));
+    s->converter = converter;
+    s->channels = channels;
+    s->last_value = (float*)calloc((size_t)channels, sizeof(float));
+    oracle_src_reset(s);
+    return s;
+}
+
+void oracle_src_delete(oracle_src* s) {
+    if (!s) return;
+    free(s->last_value);
+    free(s);
+}
+
+int oracle_src_reset(oracle_src* s) {
+    s->reset = 1;
+    memset(s->last_value, 0, sizeof(float) * (size_t)s->channels);
+    s->last_position = 0.0;
+    s->last_ratio = 0.0;
+    return 0;
+}
+
+int oracle_src_set_ratio(oracle_src* s, double ratio) {
+    if (src_bad_ratio(ratio)) return 6;
+    s->last_ratio = ratio;
+    return 0;
+}
+
+int oracle_src_process(oracle_src* s, const float* in, long in_frames, float* out,
+                       long out_frames, double ratio, long* in_used_frames, long* out_gen_frames) {
+    *in_used_frames = 0;
+    *out_gen_frames = 0;
+    if ((in == NULL && in_frames > 0) || (out == NULL && out_frames > 0)) return 4;
+    if (src_bad_ratio(ratio)) return 6;
+    if (in_frames < 0) in_frames = 0;
+    if (out_frames < 0) out_frames = 0;
+    if (s->last_ratio < (1.0 / 256.0)) s->last_ratio = ratio;
+    /* converter process loop */
+    if (in_frames <= 0) return 0;
+    const int ch = s->channels, linear = s->converter == 4;
+    if (s->reset) {
+        for (int c = 0; c < ch; c++) s->last_value[c] = in[c];
+        s->reset = 0;
+    }
+    long in_count = in_frames * ch, out_count = out_frames * ch, in_used = 0, out_gen = 0;
+    double src_ratio = s->last_ratio, input_index, rem;
+    if (src_bad_ratio(src_ratio)) return 22;
+    input_index = s->last_position;
+    while (input_index < 1.0 && out_gen < out_count) {
+        if (linear) {
+            if (in_used + ch * (1.0 + input_index) >= in_count) break;
+        } else {
+            if (in_used + ch * input_index >= in_count) break;
+        }
+        if (out_count > 0 && fabs(s->last_ratio - ratio) > 1e-20)
+            src_ratio = s->last_ratio + out_gen * (ratio - s->last_ratio) / out_count;
+        for (int c = 0; c < ch; c++) {
+            if (linear)
+                out[out_gen] = (float)(s->last_value[c] +
+                                       input_index * ((double)in[c] - s->last_value[c]));
+            else
+                out[out_gen] = s->last_value[c];
+            out_gen++;
+        }
+        input_index += 1.0 / src_ratio;
+    }
+    rem = src_fmod_one(input_index);
+    in_used += ch * lrint(input_index - rem);
+    input_index = rem;
+    while (out_gen < out_count &&
+           (linear ? in_used + ch * input_index < in_count
+                   : in_used + ch * input_index <= in_count)) {
+        if (out_count > 0 && fabs(s->last_ratio - ratio) > 1e-20)
+            src_ratio = s->last_ratio + out_gen * (ratio - s->last_ratio) / out_count;
+        for (int c = 0; c < ch; c++) {
+            /* in_used == 0 here (a 1-frame block with input_index in (0, 1), the case
+             * libsamplerate's SRC_DEBUG "Whoops" check flags): the frame before data_in[0]
+             * is last_value, where libsamplerate would read data_in[-channels]. */
+            const float left = in_used >= ch ? in[in_used - ch + c] : s->last_value[c];
+            if (linear)
+                out[out_gen] = (float)(left + input_index * ((double)in[in_used + c] - left));
+            else
+                out[out_gen] = left;
+            out_gen++;
+        }
+        input_index += 1.0 / src_ratio;
+        rem = src_fmod_one(input_index);
+        in_used += ch * lrint(input_index - rem);
+        input_index = rem;
+    }
+    if (in_used > in_count) {
+        input_index += (in_used - in_count) / ch;
+        in_used = in_count;
+    }
+    s->last_position = input_index;
+    if (in_used > 0)
+        for (int c = 0; c < ch; c++) s->last_value[c] = in[in_used - ch + c];
+    s->last_ratio = src_ratio;
+    *in_used_frames = in_used / ch;
+    *out_gen_frames = out_gen / ch;
+    return 0;
+}

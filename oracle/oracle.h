@@ -89,6 +89,22 @@ void oracle_fft_frame(const float* in, size_t n, float* out);
 size_t oracle_stft(const float* in, size_t n_in, size_t n, size_t hop, float* out,
                    size_t max_frames, int nthreads);
 
+/* ---------------- Sample-rate conversion (src/resample.rs:32-110) ----------------
+ * libsamplerate (libsamplerate-sys, a git dependency, Cargo.toml:24-26; not in this image,
+ * version unpinned) restated from its published src_zoh.c / src_linear.c / samplerate.c:
+ * src_new + src_process (argument checks, last_ratio priming) + the converter's process
+ * loop (f64 position walk, f32 samples, last_value carried across calls), src_reset,
+ * src_set_ratio.  Converter ids: 3 = ZERO_ORDER_HOLD, 4 = LINEAR (others -> error 10).
+ * Parity unpinned: no libsamplerate outputs are available here. */
+typedef struct oracle_src oracle_src;
+oracle_src* oracle_src_new(int converter, int channels, int* error);
+void oracle_src_delete(oracle_src* s);
+int  oracle_src_reset(oracle_src* s);
+int  oracle_src_set_ratio(oracle_src* s, double ratio);
+/* SRC_DATA's fields as arguments; returns the libsamplerate error code */
+int  oracle_src_process(oracle_src* s, const float* in, long in_frames, float* out,
+                        long out_frames, double ratio, long* in_used, long* out_gen);
+
 /* ---------------- Sources (src/signal/sources.rs) ------------------------------- */
 /* freq(rate, f, phase) (sources.rs:196-221 via FreqSweep::next :150-175), n samples */
 void oracle_freq(float rate, float freq, float phase, size_t n, float* out);

@@ -61,6 +61,14 @@ def lib():
                                   c_int]
         L.oracle_freq.argtypes = [c_float, c_float, c_float, c_size_t, c_void_p]
         L.oracle_u8_to_c64.argtypes = [c_void_p, c_size_t, c_void_p]
+        L.oracle_src_new.restype = c_void_p
+        L.oracle_src_new.argtypes = [c_int, c_int, POINTER(c_int)]
+        L.oracle_src_delete.argtypes = [c_void_p]
+        L.oracle_src_reset.argtypes = [c_void_p]
+        L.oracle_src_set_ratio.argtypes = [c_void_p, ctypes.c_double]
+        L.oracle_src_process.argtypes = [c_void_p, c_void_p, ctypes.c_long, c_void_p,
+                                         ctypes.c_long, ctypes.c_double,
+                                         POINTER(ctypes.c_long), POINTER(ctypes.c_long)]
         _L = L
     return _L
 
@@ -175,3 +183,40 @@ def u8_to_c64(iq_u8):
     out = np.empty(iq_u8.size // 2, np.complex64)
     lib().oracle_u8_to_c64(iq_u8.ctypes.data, out.size, out.ctypes.data)
     return out
+
+
+class SampleRate:
+    """libsamplerate ZOH / linear restatement behind SampleRate (src/resample.rs:32-110).
+
+    `process(ratio, frames)` takes a (n, channels) float32 array and returns
+    (input_frames_used, output (m, channels)), like SampleRate::process with an output
+    capacity of `out_cap` frames."""
+
+    def __init__(self, converter, channels):
+        err = c_int(0)
+        self.channels = channels
+        self.h = lib().oracle_src_new(converter, channels, ctypes.byref(err))
+        if not self.h:
+            raise ValueError(f"oracle_src_new: libsamplerate error {err.value}")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_src_delete(self.h)
+            self.h = None
+
+    def reset(self):
+        lib().oracle_src_reset(self.h)
+
+    def set_ratio(self, ratio):
+        return lib().oracle_src_set_ratio(self.h, ratio)
+
+    def process(self, ratio, frames, out_cap):
+        x = np.ascontiguousarray(frames, np.float32).reshape(-1, self.channels)
+        out = np.zeros((max(out_cap, 1), self.channels), np.float32)
+        used, gen = ctypes.c_long(0), ctypes.c_long(0)
+        rc = lib().oracle_src_process(self.h, x.ctypes.data if x.size else None, x.shape[0],
+                                      out.ctypes.data, out_cap, ratio, ctypes.byref(used),
+                                      ctypes.byref(gen))
+        if rc:
+            raise ValueError(f"oracle_src_process: libsamplerate error {rc}")
+        return used.value, out[:gen.value].copy()

@@ -1,0 +1,216 @@
+"""Sample-rate conversion: resample::SampleRate (src/resample.rs:32-110) over libsamplerate's
+zero-order-hold / linear converters, and the adapters::Resample Signal stage
+(src/signal/adapters/resample.rs:17-82).
+
+Oracle: oracle_src_* (oracle/oracle.c), a restatement of libsamplerate's samplerate.c /
+src_zoh.c / src_linear.c.  libsamplerate itself is a git dependency (Cargo.toml:24-26) that
+is not in this image and the reference holds no resampler outputs, so the restatement is
+"parity unpinned" against libsamplerate; it is pinned here by known-answer streams (ratio
+1 = one-frame delay, 2x linear = midpoints, 1/2 = every other frame) and by block-partition
+invariance.  GPU vs oracle: bit-exact (array_equal) outputs and identical frame counts.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+LINEAR, ZOH = 4, 3
+
+
+# ----------------------------- CPU: oracle KATs -------------------------------------
+def test_oracle_known_answers(oracle):
+    x = np.arange(1, 11, dtype=np.float32)
+    s = oracle.SampleRate(LINEAR, 1)
+    used, y = s.process(1.0, x, 100)
+    assert used == 10 and np.array_equal(y.ravel(), np.r_[1, x[:-1]])  # one-frame delay
+    used, y = s.process(1.0, x + 10, 100)
+    assert np.array_equal(y.ravel(), np.r_[10, x[:-1] + 10])
+    s = oracle.SampleRate(LINEAR, 1)
+    used, y = s.process(2.0, x, 100)
+    assert np.array_equal(y.ravel()[3:], np.arange(1.5, 10, 0.5, dtype=np.float32))
+    s = oracle.SampleRate(ZOH, 1)
+    used, y = s.process(0.5, x, 100)
+    assert np.array_equal(y.ravel(), [1, 2, 4, 6, 8, 10])
+
+
+@pytest.mark.parametrize("conv", [ZOH, LINEAR], ids=["zoh", "linear"])
+@pytest.mark.parametrize("ratio", [48000 * 3.0 / 1.8e6, 0.75, 1.0, 2.5, 48000 / 44100])
+def test_oracle_partition_invariance(oracle, conv, ratio):
+    """Whole-stream output does not depend on how the input is split into calls."""
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((3000, 2)).astype(np.float32)
+    a = oracle.SampleRate(conv, 2)
+    _, ya = a.process(ratio, x, 100000)
+    b = oracle.SampleRate(conv, 2)
+    outs, i = [], 0
+    while i < x.shape[0]:
+        n = int(rng.integers(1, 400))
+        used, y = b.process(ratio, x[i:i + n], 100000)
+        outs.append(y)
+        i += used
+    yb = np.concatenate(outs)
+    m = min(len(ya), len(yb))
+    assert abs(len(ya) - len(yb)) <= 1 and np.array_equal(ya[:m], yb[:m])
+
+
+def test_oracle_linear_on_a_line(oracle):
+    """Linear interpolation of a straight line stays on the line (up to f32 rounding)."""
+    x = (0.25 * np.arange(5000)).astype(np.float32)
+    s = oracle.SampleRate(LINEAR, 1)
+    used, y = s.process(1.37, x, 100000)
+    d = np.diff(y.ravel()[2:].astype(np.float64))
+    assert np.allclose(d, 0.25 / 1.37, atol=2e-3)
+
+
+# ----------------------------- CPU: ABI rejections ----------------------------------
+def test_src_abi_without_device(sdr):
+    L = sdr.lib()
+    err = ctypes.c_int(0)
+    assert not L.sdrgpu_src_new(0, 2, 1, ctypes.byref(err)) and err.value == 10  # sinc
+    assert not L.sdrgpu_src_new(0, 9, 1, ctypes.byref(err)) and err.value == 10
+    assert not L.sdrgpu_src_new(0, 4, 0, ctypes.byref(err)) and err.value == 11
+    assert L.sdrgpu_src_get_channels(None) == -2
+    assert L.sdrgpu_src_process(None, None) == 2
+    assert L.sdrgpu_src_set_ratio(None, 1.0) == 2
+    assert L.sdrgpu_src_delete(None) is None
+    assert L.sdrgpu_src_strerror(6) == b"SRC ratio outside [1/256, 256] range."
+    assert L.sdrgpu_src_strerror(99) is None
+    assert L.sdrgpu_src_get_name(4) == b"Linear Interpolator"
+    assert L.sdrgpu_src_get_name(5) is None
+    from sdrgpu import resample
+    assert resample.ConverterType.ZeroOrderHold.name_() == "ZOH Interpolator"
+    assert str(resample.Error(16)).startswith("DataOverlap")
+
+
+# ----------------------------- GPU parity -------------------------------------------
+def _run_both(sdr, oracle, conv, ch, ratio, x, rng, split=True, out_cap=None):
+    from sdrgpu import resample
+    g = resample.SampleRate(conv, ch)
+    o = oracle.SampleRate(conv, ch)
+    i, n, stalls = 0, x.shape[0], 0
+    gy = []
+    while i < n and stalls < 20:
+        m = int(rng.integers(1, 700)) if split else n - i
+        cap = out_cap if out_cap is not None else int(rng.integers(1, 2000))
+        gu, ga = g.process(ratio, x[i:i + m], cap)
+        ou, oa = o.process(ratio, x[i:i + m], cap)
+        assert gu == ou and ga.shape == oa.shape, (i, m, cap, gu, ou, ga.shape, oa.shape)
+        assert np.array_equal(ga, oa), (i, m, cap)
+        gy.append(ga)
+        i += gu
+        stalls = stalls + 1 if gu == 0 and ga.shape[0] == 0 else 0
+    assert i >= n
+    gu, ga = g.process(ratio, x[:0], 100)  # end of input (empty block): nothing
+    assert gu == 0 and ga.shape[0] == 0
+    return g, o, np.concatenate(gy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conv", [ZOH, LINEAR], ids=["zoh", "linear"])
+@pytest.mark.parametrize("ratio", [1.0, 2.0, 0.5, 48000 * 3.0 / 1.8e6, 48000 / 144000.0,
+                                   48000 / 44100, 7.3, 1 / 255.0, 256.0])
+@pytest.mark.parametrize("ch", [1, 2, 6])
+def test_src_bit_exact(sdr, oracle, conv, ratio, ch):
+    rng = np.random.default_rng(int(ratio * 1000) + ch * 7 + conv)
+    x = rng.standard_normal((3001, ch)).astype(np.float32)
+    _run_both(sdr, oracle, conv, ch, ratio, x, rng)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conv", [ZOH, LINEAR], ids=["zoh", "linear"])
+def test_src_many_channels_one_shot(sdr, oracle, conv):
+    """A batch of 1024 complex streams sharing one ratio = 2048 interleaved channels."""
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((4096, 2048)).astype(np.float32)
+    _run_both(sdr, oracle, conv, 2048, 48000 * 3.0 / 1.8e6 * 7, x, rng, split=False,
+              out_cap=1 << 16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("conv", [ZOH, LINEAR], ids=["zoh", "linear"])
+def test_src_variable_ratio_reset_clone(sdr, oracle, conv):
+    from sdrgpu import resample
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((6000, 2)).astype(np.float32)
+    g = resample.SampleRate(conv, 2)
+    o = oracle.SampleRate(conv, 2)
+    i = 0
+    for step, ratio in enumerate([1.0, 1.3, 0.4, 0.4, 3.0, 0.9]):
+        if step == 3:
+            assert g.set_ratio(0.7) is None and o.set_ratio(0.7) == 0
+        if step == 4:
+            g.reset()
+            o.reset()
+        gu, ga = g.process(ratio, x[i:i + 900], 1500)
+        ou, oa = o.process(ratio, x[i:i + 900], 1500)
+        assert gu == ou and np.array_equal(ga, oa), step
+        i += gu
+    # clone carries position, ratio and last_value
+    c = g.try_clone()
+    gu, ga = c.process(0.9, x[i:i + 500], 2000)
+    ou, oa = o.process(0.9, x[i:i + 500], 2000)
+    assert gu == ou and np.array_equal(ga, oa)
+    assert c.channels() == 2
+
+
+@pytest.mark.gpu
+def test_src_errors_and_empty(sdr):
+    from sdrgpu import resample
+    L = sdr.lib()
+    g = resample.SampleRate(resample.ConverterType.Linear, 1)
+    with pytest.raises(resample.Error) as e:
+        g.process(300.0, np.ones(10, np.float32), 10)
+    assert e.value.code == 6
+    with pytest.raises(resample.Error) as e:
+        g.set_ratio(1e-3)
+    assert e.value.code == 6
+    used, y = g.process(1.0, np.zeros(0, np.float32), 10)  # end of input: nothing
+    assert used == 0 and y.shape[0] == 0
+    buf = np.ones(64, np.float32)  # data_in overlapping data_out
+    d = resample.SrcData(buf.ctypes.data, buf.ctypes.data + 16, 8, 8, 0, 0, 0, 1.0)
+    assert L.sdrgpu_src_process(g.h, ctypes.byref(d)) == 16
+
+
+@pytest.mark.gpu
+def test_src_process_dev(sdr, oracle):
+    from sdrgpu import device, resample
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((20000, 2)).astype(np.float32)
+    ratio = 48000 / 1.8e6 * 3
+    g = resample.SampleRate(resample.ConverterType.Linear, 2)
+    o = oracle.SampleRate(LINEAR, 2)
+    din = device.DeviceBuffer.from_numpy(x)
+    dout = device.DeviceBuffer(8 * 20000)
+    used, gen = g.process_dev(ratio, din.ptr, 20000, dout.ptr, 20000)
+    g.sync()
+    ou, oa = o.process(ratio, x, 20000)
+    assert used == ou and gen == oa.shape[0]
+    assert np.array_equal(dout.download(gen * 2, np.float32).reshape(-1, 2), oa)
+
+
+@pytest.mark.gpu
+def test_signal_resample_with_matches_adapter(sdr, oracle):
+    """fm.resample_with(SincFastest -> Linear here, 144 kHz) from 1.8 Msps (src/main.rs:50)."""
+    from sdrgpu import resample, signal
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal(50000).astype(np.float32)
+    got = signal.from_array(1.8e6, x, block=7000).resample_with(
+        resample.ConverterType.Linear, 48000.0 * 3.0)
+    assert got.rate() == 144000.0
+    y = got.collect()
+    # the adapter's loop (adapters/resample.rs:36-82) on the oracle
+    o = oracle.SampleRate(LINEAR, 1)
+    ratio = float(np.float32(144000.0)) / float(np.float32(1.8e6))
+    buf, ref, i = np.zeros(0, np.float32), [], 0
+    while True:
+        take = 4096 - buf.size
+        buf = np.concatenate([buf, x[i:i + take]])
+        i += min(take, max(0, x.size - i))
+        used, out = o.process(ratio, buf, 4096)
+        if buf.size == 0 and out.shape[0] == 0:
+            break
+        buf = buf[used:]
+        ref.append(out.ravel())
+    assert np.array_equal(y, np.concatenate(ref))
+    with pytest.raises(resample.Error):
+        signal.from_array(1.8e6, x).resample(48000.0).collect()

@@ -152,6 +152,21 @@ SIGNATURES = [
     ("sdrgpu_biquad_reset", c_int, [_H]),
     ("sdrgpu_biquad_clone", c_int, [_H, _PH]),
     ("sdrgpu_biquad_destroy", None, [_H]),
+    # sample-rate conversion (libsamplerate surface; returns libsamplerate codes)
+    ("sdrgpu_src_new", c_void_p, [c_int, c_int, c_int, POINTER(c_int)]),
+    ("sdrgpu_src_process", c_int, [_H, c_void_p]),
+    ("sdrgpu_src_process_dev", c_int, [_H, c_void_p]),
+    ("sdrgpu_src_sync", c_int, [_H]),
+    ("sdrgpu_src_reset", c_int, [_H]),
+    ("sdrgpu_src_clone", c_void_p, [_H, POINTER(c_int)]),
+    ("sdrgpu_src_get_channels", c_int, [_H]),
+    ("sdrgpu_src_set_ratio", c_int, [_H, ctypes.c_double]),
+    ("sdrgpu_src_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_src_delete", c_void_p, [_H]),
+    ("sdrgpu_src_strerror", c_char_p, [c_int]),
+    ("sdrgpu_src_get_name", c_char_p, [c_int]),
+    ("sdrgpu_src_get_description", c_char_p, [c_int]),
+    ("sdrgpu_src_get_version", c_char_p, []),
     # multi-GPU fan-out / gather (RCCL)
     ("sdrgpu_comm_unique_id", c_int, [c_void_p]),
     ("sdrgpu_comm_init", c_int, [c_int, c_int, c_int, c_void_p, _PH]),

@@ -14,6 +14,9 @@ reference names and argument meaning:
                      is fused into the FIR kernel (only kept outputs are computed).
   window(duration)   Window (adapters/mod.rs:270-303), cap = round(duration * rate)
   .decimate(..).map(fft)  the live.rs STFT pattern -> one GPU Stft stage
+  resample(rate), resample_with(typ, rate)
+                     adapters::Resample (adapters/resample.rs:17-82): 4096-frame buffers
+                     through resample.SampleRate (GPU ZOH / linear); rate() = the new rate
   map(f), take(duration), skip(duration), iter(), collect()
 
 Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), impulse
@@ -28,6 +31,7 @@ import numpy as np
 from . import _lib
 from . import filter as _filter
 from . import fft as _fft
+from . import resample as _resample
 
 DEFAULT_BLOCK = 1 << 16
 
@@ -107,6 +111,62 @@ class Signal:
                 yield b[first::wait]
                 phase = (phase + len(b)) % wait
         return Signal(self._rate, gen, self.sample_kind)  # Decimate::rate quirk (:38-40)
+
+    def resample(self, rate: float) -> "Signal":
+        """Signal::resample (src/signal/mod.rs:78-84): SincBestQuality, which this build
+        rejects with resample.Error(BadConverter) when the stream starts."""
+        return self.resample_with(_resample.ConverterType.SincBestQuality, rate)
+
+    def resample_with(self, typ, rate: float) -> "Signal":
+        """Signal::resample_with -> adapters::Resample (adapters/resample.rs:17-82): refill a
+        4096-frame buffer from upstream, SampleRate::process(ratio, buffer, capacity 4096),
+        drop the used frames, stop when a call has neither input nor output."""
+        up = self
+        buffer_size = 4096
+        # ratio: rate as f64 / signal.rate() as f64, both f32 in the reference
+        ratio = float(np.float32(rate)) / float(np.float32(up.rate()))
+
+        def gen():
+            sr = None
+            buf = None
+            cplx = False
+            it = iter(up.blocks())
+            pending = []  # upstream frames not yet in the buffer
+            exhausted = False
+            while True:
+                while not exhausted and (buf is None or buf.shape[0] < buffer_size):
+                    if pending:
+                        need = buffer_size - (0 if buf is None else buf.shape[0])
+                        take, rest = pending[0][:need], pending[0][need:]
+                        buf = take if buf is None else np.concatenate([buf, take])
+                        pending = [rest] if rest.shape[0] else []
+                        continue
+                    b = next(it, None)
+                    if b is None:
+                        exhausted = True
+                        break
+                    b = np.asarray(b)
+                    if sr is None:
+                        cplx = np.iscomplexobj(b)
+                        ch = 2 if cplx else (1 if b.ndim == 1 else b.shape[1])
+                        sr = _resample.SampleRate(typ, ch)
+                    pending.append(_resample._frames(b, sr.channels()))
+                if sr is None:
+                    return
+                if buf is None:
+                    buf = np.zeros((0, sr.channels()), np.float32)
+                used, out = sr.process(ratio, buf, buffer_size)
+                if buf.shape[0] == 0 and out.shape[0] == 0:
+                    return
+                buf = buf[used:]
+                if out.shape[0]:
+                    if cplx:
+                        yield out.view(np.complex64).reshape(-1)
+                    elif out.shape[1] == 1:
+                        yield out.reshape(-1)
+                    else:
+                        yield out
+        return Signal(float(np.float32(rate)), gen, self.sample_kind)
 
     def window(self, duration: float) -> "Signal":
         cap = int(round(duration * self._rate))
