@@ -38,7 +38,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "all"])
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "src", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -284,12 +284,41 @@ def bench_c5(args):
     return res if rank == 0 else None
 
 
+# ------------------------------------------------------------------------------ src
+def bench_src(args):
+    import sdrgpu
+    from sdrgpu import resample
+    from sdrgpu.device import DeviceBuffer, synchronize
+    ch, nf = 2048, 1 << 16
+    ratio = float(np.float32(144000.0)) / float(np.float32(1.8e6))
+    g = resample.SampleRate(resample.ConverterType.Linear, ch)
+    x = DeviceBuffer.empty(nf * ch // 2)
+    fill(x, nf * ch // 2, 13)
+    out_cap = int(nf * ratio) + 16
+    y = DeviceBuffer.empty(out_cap * ch // 2)
+    gen = [0]
+
+    def step():
+        g.reset()
+        gen[0] = g.process_dev(ratio, x.ptr, nf, y.ptr, out_cap)[1]
+
+    wall, ms = time_events(step, g.stream(), args.steps, args.warmup,
+                           lambda: (g.sync(), synchronize()))
+    nout = gen[0]
+    return {"config": "src: linear resampler 1.8 Msps -> 144 kHz (ratio 0.08), 1024 complex "
+                      "streams = 2048 interleaved channels x 2^16 frames",
+            "metric": "input Msamples/s (all channels)", "value": round(nf * ch / (ms * 1e-3) / 1e6, 1),
+            "wall_value": round(nf * ch / wall / 1e6, 1),
+            "output_frames": nout, "wall_ms_per_step": round(wall * 1e3, 3),
+            "roofline_kernel_estimate": roof(12, nout * ch, ms)}
+
+
 def main():
     args = parse()
-    todo = ["c3", "c4", "c5", "c2u8", "c2host"] if args.config == "all" else [args.config]
+    todo = ["c3", "c4", "c5", "c2u8", "c2host", "src"] if args.config == "all" else [args.config]
     for c in todo:
         r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
-             "c2host": bench_c2host}[c](args)
+             "c2host": bench_c2host, "src": bench_src}[c](args)
         if r is not None:
             print(json.dumps(r), flush=True)
 

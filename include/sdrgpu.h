@@ -318,6 +318,7 @@ sdrgpu_src_state* sdrgpu_src_clone(sdrgpu_src_state* s, int* error);
 int sdrgpu_src_get_channels(sdrgpu_src_state* s);   /* negative error code on a null handle */
 int sdrgpu_src_set_ratio(sdrgpu_src_state* s, double new_ratio);
 int sdrgpu_src_set_stream(sdrgpu_src_state* s, void* hip_stream);
+int sdrgpu_src_get_stream(sdrgpu_src_state* s, void** hip_stream);
 sdrgpu_src_state* sdrgpu_src_delete(sdrgpu_src_state* s);  /* returns NULL, as src_delete */
 const char* sdrgpu_src_strerror(int error);
 const char* sdrgpu_src_get_name(int converter_type);        /* NULL for unknown ids */

@@ -394,6 +394,12 @@ int sdrgpu_src_set_stream(sdrgpu_src_state* s, void* hip_stream) {
     return 0;
 }
 
+int sdrgpu_src_get_stream(sdrgpu_src_state* s, void** hip_stream) {
+    if (!s || !hip_stream) return SDRGPU_SRC_ERR_BAD_STATE;
+    *hip_stream = s->stream.cur;
+    return 0;
+}
+
 sdrgpu_src_state* sdrgpu_src_delete(sdrgpu_src_state* s) {
     if (s) {
         (void)sdrgpu_src_sync(s);

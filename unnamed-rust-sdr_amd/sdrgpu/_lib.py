@@ -162,6 +162,7 @@ SIGNATURES = [
     ("sdrgpu_src_get_channels", c_int, [_H]),
     ("sdrgpu_src_set_ratio", c_int, [_H, ctypes.c_double]),
     ("sdrgpu_src_set_stream", c_int, [_H, c_void_p]),
+    ("sdrgpu_src_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_src_delete", c_void_p, [_H]),
     ("sdrgpu_src_strerror", c_char_p, [c_int]),
     ("sdrgpu_src_get_name", c_char_p, [c_int]),

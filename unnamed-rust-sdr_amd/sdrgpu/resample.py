@@ -116,6 +116,11 @@ class SampleRate:
         Error.result(lib().sdrgpu_src_process_dev(self.h, ctypes.byref(d)))
         return d.input_frames_used, d.output_frames_gen
 
+    def stream(self) -> int:
+        p = c_void_p()
+        Error.result(lib().sdrgpu_src_get_stream(self.h, ctypes.byref(p)))
+        return p.value or 0
+
     def sync(self):
         Error.result(lib().sdrgpu_src_sync(self.h))
 
