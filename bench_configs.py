@@ -298,8 +298,7 @@ def bench_src(args):
     y = DeviceBuffer.empty(out_cap * ch // 2)
     gen = [0]
 
-    def step():
-        g.reset()
+    def step():  # state carries from call to call, as in a stream
         gen[0] = g.process_dev(ratio, x.ptr, nf, y.ptr, out_cap)[1]
 
     wall, ms = time_events(step, g.stream(), args.steps, args.warmup,

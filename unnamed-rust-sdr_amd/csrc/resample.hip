@@ -18,27 +18,78 @@ namespace sdrgpu {
 namespace {
 
 constexpr int kSrcBlock = 256;
+constexpr int kSrcRows = 4;  // frames per workgroup in the wide-frame kernel
 
 template <bool LINEAR>
+__device__ __forceinline__ float src_eval(const float* __restrict__ in, long channels, int l,
+                                          double f, long ch, const float* __restrict__ lv) {
+    const float a = l < 0 ? lv[ch] : in[(long)l * channels + ch];
+    if constexpr (LINEAR) {
+        const float b = in[((long)l + 1) * channels + ch];
+        const double da = (double)a;
+        return (float)__dadd_rn(da, __dmul_rn(f, __dsub_rn((double)b, da)));
+    } else {
+        return a;
+    }
+}
+
+// Wide frames (channels >= 64, e.g. a batch of streams): blockIdx.x = a run of kSrcRows
+// output frames, blockIdx.y tiles the channels of a frame; the (left, frac) of a frame is
+// uniform across the workgroup (scalar loads), every sample load / store is coalesced.
+template <bool LINEAR>
+__global__ __launch_bounds__(kSrcBlock) void src_interp_wide_kernel(
+    const float* __restrict__ in, long channels, const int* __restrict__ left,
+    const double* __restrict__ frac, long nframes, const float* __restrict__ last_value,
+    float* __restrict__ out) {
+    const long ch = (long)blockIdx.y * kSrcBlock + threadIdx.x;
+    const long k0 = (long)blockIdx.x * kSrcRows;
+    if (ch >= channels) return;
+#pragma unroll
+    for (int r = 0; r < kSrcRows; ++r) {
+        const long k = k0 + r;
+        if (k >= nframes) break;
+        out[k * channels + ch] =
+            src_eval<LINEAR>(in, channels, left[k], LINEAR ? frac[k] : 0.0, ch, last_value);
+    }
+}
+
+// Narrow frames (1..63 channels): one sample per lane over the flattened (frame, channel)
+// index; CH > 0 fixes the channel count at compile time (1 = f32, 2 = Complex<f32>).
+template <bool LINEAR, int CH>
 __global__ __launch_bounds__(kSrcBlock) void src_interp_kernel(
     const float* __restrict__ in, long channels, const int* __restrict__ left,
     const double* __restrict__ frac, long nframes, const float* __restrict__ last_value,
     float* __restrict__ out) {
-    const long total = nframes * channels;
+    const long C = CH > 0 ? CH : channels;
+    const long total = nframes * C;
     const long stride = (long)gridDim.x * kSrcBlock;
     for (long t = (long)blockIdx.x * kSrcBlock + threadIdx.x; t < total; t += stride) {
-        const long k = t / channels;
-        const long ch = t - k * channels;
-        const int l = left[k];
-        const float a = l < 0 ? last_value[ch] : in[(long)l * channels + ch];
-        if constexpr (LINEAR) {
-            const float b = in[((long)l + 1) * channels + ch];
-            const double da = (double)a;
-            out[t] = (float)__dadd_rn(da, __dmul_rn(frac[k], __dsub_rn((double)b, da)));
-        } else {
-            out[t] = a;
-        }
+        const long k = CH > 0 ? t / CH : (long)((unsigned long)t / (unsigned long)C);
+        const long ch = t - k * C;
+        out[t] = src_eval<LINEAR>(in, C, left[k], LINEAR ? frac[k] : 0.0, ch, last_value);
     }
+}
+
+template <bool LINEAR>
+void src_launch_t(const float* in, long channels, const int* left, const double* frac,
+                  long nframes, const float* lv, float* out, hipStream_t s) {
+    if (channels >= 64) {
+        const dim3 grid((unsigned)((nframes + kSrcRows - 1) / kSrcRows),
+                        (unsigned)((channels + kSrcBlock - 1) / kSrcBlock));
+        src_interp_wide_kernel<LINEAR><<<grid, kSrcBlock, 0, s>>>(in, channels, left, frac,
+                                                                  nframes, lv, out);
+        return;
+    }
+    long blocks = (nframes * channels + kSrcBlock - 1) / kSrcBlock;
+    if (blocks > 65536) blocks = 65536;
+    const unsigned g = (unsigned)blocks;
+    if (channels == 1)
+        src_interp_kernel<LINEAR, 1><<<g, kSrcBlock, 0, s>>>(in, 1, left, frac, nframes, lv, out);
+    else if (channels == 2)
+        src_interp_kernel<LINEAR, 2><<<g, kSrcBlock, 0, s>>>(in, 2, left, frac, nframes, lv, out);
+    else
+        src_interp_kernel<LINEAR, 0><<<g, kSrcBlock, 0, s>>>(in, channels, left, frac, nframes,
+                                                             lv, out);
 }
 
 }  // namespace
@@ -46,16 +97,14 @@ __global__ __launch_bounds__(kSrcBlock) void src_interp_kernel(
 int src_interp_launch(bool linear, const float* in, long channels, const int* left,
                       const double* frac, long nframes, const float* last_value, float* out,
                       hipStream_t s) {
-    const long total = nframes * channels;
-    if (total <= 0) return SDRGPU_OK;
-    long blocks = (total + kSrcBlock - 1) / kSrcBlock;
-    if (blocks > 65536) blocks = 65536;
+    if (nframes <= 0 || channels <= 0) return SDRGPU_OK;
+    if ((nframes + kSrcRows - 1) / kSrcRows > 0x7fffffffL ||
+        (channels + kSrcBlock - 1) / kSrcBlock > 65535)
+        return SDRGPU_ERR_UNSUPPORTED;
     if (linear)
-        src_interp_kernel<true><<<(unsigned)blocks, kSrcBlock, 0, s>>>(in, channels, left, frac,
-                                                                       nframes, last_value, out);
+        src_launch_t<true>(in, channels, left, frac, nframes, last_value, out, s);
     else
-        src_interp_kernel<false><<<(unsigned)blocks, kSrcBlock, 0, s>>>(in, channels, left, frac,
-                                                                        nframes, last_value, out);
+        src_launch_t<false>(in, channels, left, frac, nframes, last_value, out, s);
     return hipGetLastError() == hipSuccess ? SDRGPU_OK : SDRGPU_ERR_LAUNCH;
 }
 
