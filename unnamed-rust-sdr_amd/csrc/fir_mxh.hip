@@ -197,7 +197,8 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 
 // ABL (debug ablation, results invalid): 1 = memory only (no LDS reads / MFMA),
 // 2 = no HBM loads (compute only)
-// NT: bit 0 = non-temporal sample loads, bit 1 = non-temporal output stores
+// NT: bit 0 = non-temporal sample loads, bit 1 = non-temporal output stores, bit 2 =
+// line-complete output stores (lane-pair half swap)
 // U8: interleaved u8 I/Q input (rtl_tcp ingest fused into the load, 2 B per sample); the
 // samples are exact integers after a fixed x128 scale, so no per-tile scale, no lo planes,
 // 2 MFMAs per component per chunk.
@@ -443,7 +444,32 @@ void fir_mxh_kernel(MxhParams p) {
                 yr[i] = __builtin_amdgcn_ldexpf(cr[i], so);
                 yi[i] = __builtin_amdgcn_ldexpf(ci[i], so);
             }
-            if (p.vec_out && (t0 + t + 1) * kTileOut <= p.n_out) {
+            if (p.vec_out && (t0 + t + 1) * kTileOut <= p.n_out && (NT & 4)) {
+                // Line-complete stores: the 16 outputs (128 B) of a block sit in 4 lanes, so a
+                // plain 16-B store covers only half of each line per instruction.  Blocks
+                // 2j / 2j+1 (lanes l, l ^ PX) swap one half: then instruction 1 writes block
+                // 2j's whole line from 8 lanes and instruction 2 block 2j+1's.
+                constexpr int PX = D == 4 ? 4 : 1;  // sigma pairs v / v^4; D = 1: v / v^1
+                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                const bool even = (sv & 1) == 0;
+                const f32x4 snd = even ? y1 : y0;
+                f32x4 rcv;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    rcv[i] = __shfl_xor(snd[i], PX);
+                f32x4* o1 = reinterpret_cast<f32x4*>(out + (even ? m : m - 14));
+                f32x4* o2 = reinterpret_cast<f32x4*>(out + (even ? m + 16 : m + 2));
+                const f32x4 s1 = even ? y0 : rcv;
+                const f32x4 s2 = even ? rcv : y1;
+                if (NT & 2) {
+                    __builtin_nontemporal_store(s1, o1);
+                    __builtin_nontemporal_store(s2, o2);
+                } else {
+                    *o1 = s1;
+                    *o2 = s2;
+                }
+            } else if (p.vec_out && (t0 + t + 1) * kTileOut <= p.n_out) {
                 f32x4* o4 = reinterpret_cast<f32x4*>(out + m);
                 const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
                 const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
@@ -576,12 +602,14 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                        (size_t)kWaves * (GeoH<CC, DD>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
-        if (u8) SDRGPU_MXH_GO(CC, 0, 3, true, 4);                                              \
+        if (u8 && nt == 7) SDRGPU_MXH_GO(CC, 0, 7, true, 4);                                  \
+        else if (u8) SDRGPU_MXH_GO(CC, 0, 3, true, 4);                                         \
         else if (abl == 1) SDRGPU_MXH_GO(CC, 1, 0, false, 4);                                  \
         else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 0, false, 4);                                  \
         else if (nt == 1) SDRGPU_MXH_GO(CC, 0, 1, false, 4);                                   \
         else if (nt == 2) SDRGPU_MXH_GO(CC, 0, 2, false, 4);                                   \
         else if (nt == 3) SDRGPU_MXH_GO(CC, 0, 3, false, 4);                                   \
+        else if (nt == 7) SDRGPU_MXH_GO(CC, 0, 7, false, 4);                                   \
         else SDRGPU_MXH_GO(CC, 0, 0, false, 4);                                                \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
@@ -590,6 +618,7 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     if (D == 1 && NCH == CC) {                                                                 \
         if (abl == 1) SDRGPU_MXH_GO(CC, 1, 3, false, 1);                                       \
         else if (abl == 2) SDRGPU_MXH_GO(CC, 2, 3, false, 1);                                  \
+        else if (nt == 7) SDRGPU_MXH_GO(CC, 0, 7, false, 1);                                   \
         else SDRGPU_MXH_GO(CC, 0, 3, false, 1);                                                \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
