@@ -38,7 +38,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "src", "all"])
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -165,6 +165,43 @@ def bench_c2host(args):
             "metric": "complex Msamples/s (input, PCIe-inclusive)", "value": round(n / el / 1e6, 1),
             "wall_ms_per_call": round(el * 1e3, 3),
             "host_bytes_per_s": round(10 * n / el / 1e9, 2)}
+
+
+# ------------------------------------------------------------------------------ c2pinned
+def bench_c2pinned(args):
+    """configs[1] streamed from HOST memory the way the Block adapter would
+    (src/signal/adapters/block.rs:105-207): two pinned input/output block pairs, each block
+    enqueued with sdrgpu_fir_process_async (H2D + FIR + D2H, no wait) so block i+1's
+    transfer queues behind block i's; C64 samples and rtl_tcp u8 bytes."""
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import PinnedBuffer
+    n = 1 << 24  # samples per block
+    nblocks = 16
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    res = {"config": "c2pinned: configs[1] from pinned host blocks of 2^24 samples, async "
+                     "H2D + FIR + D2H, 2 blocks in flight (PCIe-inclusive)"}
+    for kind, name, ib in ((sdrgpu.C64, "c64", 8), (sdrgpu.CU8, "u8", 2)):
+        fir = sdrgpu.filter.Fir(taps, decim=4, sample_kind=kind).design(2.4e6)
+        ins = [PinnedBuffer(n * ib, np.uint8) for _ in range(2)]
+        outs = [PinnedBuffer(n // 4, np.complex64) for _ in range(2)]
+        pat = np.random.default_rng(6).integers(0, 256, size=n * ib, dtype=np.uint8)
+        for b in ins:
+            b.array[:] = pat
+        for i in range(2):  # warm-up (staging buffers)
+            fir.process_async(ins[i].ptr, n, outs[i].ptr, n // 4)
+        fir.sync()
+        t0 = time.perf_counter()
+        for i in range(nblocks):
+            assert fir.process_async(ins[i & 1].ptr, n, outs[i & 1].ptr, n // 4) == n // 4
+        fir.sync()
+        el = (time.perf_counter() - t0) / nblocks
+        res[name] = {"value": round(n / el / 1e6, 1), "unit": "complex Msamples/s (input)",
+                     "ms_per_block": round(el * 1e3, 3),
+                     "host_bytes_per_s_GB": round((ib + 2) * n / el / 1e9, 2)}
+        for b in ins + outs:
+            b.free()
+    return res
 
 
 # ------------------------------------------------------------------------------ c4
@@ -314,10 +351,10 @@ def bench_src(args):
 
 def main():
     args = parse()
-    todo = ["c3", "c4", "c5", "c2u8", "c2host", "src"] if args.config == "all" else [args.config]
+    todo = ["c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src"] if args.config == "all" else [args.config]
     for c in todo:
         r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
-             "c2host": bench_c2host, "src": bench_src}[c](args)
+             "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src}[c](args)
         if r is not None:
             print(json.dumps(r), flush=True)
 

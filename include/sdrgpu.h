@@ -81,6 +81,10 @@ int sdrgpu_device_count(int* count);
 enum sdrgpu_copy_kind { SDRGPU_H2D = 0, SDRGPU_D2H = 1, SDRGPU_D2D = 2 };
 int sdrgpu_dev_alloc(int device, size_t bytes, void** dptr);
 int sdrgpu_dev_free(int device, void* dptr);
+/* Pinned (page-locked) host memory for the *_async entry points: copies from/to it are DMA
+ * straight from the caller's buffer and do not block the calling thread. */
+int sdrgpu_host_alloc(int device, size_t bytes, void** hptr);
+int sdrgpu_host_free(void* hptr);
 int sdrgpu_dev_copy(int device, void* dst, const void* src, size_t bytes, int kind);
 int sdrgpu_dev_memset(int device, void* dptr, int value, size_t bytes);
 int sdrgpu_dev_synchronize(int device);
@@ -126,6 +130,14 @@ int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
                        size_t out_cap, size_t* n_out);
 int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d_out,
                            size_t out_cap, size_t* n_out);
+/* HOST pointers, asynchronous (the Block adapter's producer/consumer split,
+ * src/signal/adapters/block.rs:105-207): H2D + FIR + D2H are enqueued on the handle's
+ * stream and the call returns with *n_out set.  Use pinned buffers (sdrgpu_host_alloc) --
+ * pageable ones work but the copies then block -- keep `in` unchanged and read `out` only
+ * after sdrgpu_fir_sync.  Double-buffering two blocks keeps PCIe busy in both directions
+ * of the pipeline while the host prepares the next block. */
+int sdrgpu_fir_process_async(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
+                             size_t out_cap, size_t* n_out);
 int sdrgpu_fir_sync(sdrgpu_fir* h);
 int sdrgpu_fir_reset(sdrgpu_fir* h);                           /* FilterDesign::design -> fresh state */
 int sdrgpu_fir_clone(const sdrgpu_fir* h, sdrgpu_fir** out);   /* #[derive(Clone)] Fir, fir.rs:6 */

@@ -63,6 +63,25 @@ int sdrgpu_dev_alloc(int device, size_t bytes, void** dptr) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_host_alloc(int device, size_t bytes, void** hptr) {
+    using namespace sdrgpu::detail;
+    if (!hptr) return SDRGPU_ERR_INVALID;
+    *hptr = nullptr;
+    int st = check_device(device);
+    if (st) return st;
+    DeviceGuard g(device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return SDRGPU_ERR_NOMEM;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_host_free(void* hptr) {
+    if (!hptr) return SDRGPU_OK;
+    SDRGPU_HIP_TRY(hipHostFree(hptr));
+    return SDRGPU_OK;
+}
+
 int sdrgpu_dev_free(int device, void* dptr) {
     using namespace sdrgpu::detail;
     if (!dptr) return SDRGPU_OK;

@@ -43,6 +43,13 @@ struct FirCore {
     int os_status = SDRGPU_OK;
     void* mx_state = nullptr;              // split-bf16 MFMA direct-form plan (lazily built)
     int mx_status = SDRGPU_OK;
+    // async host streaming: downloads on their own stream (block i's D2H overlaps block
+    // i+1's H2D -- PCIe is full duplex), two output slots guarded by events
+    hipStream_t d2h = nullptr;
+    hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_o[2] = {nullptr, nullptr};
+    bool ev_o_live[2] = {false, false};
+    DevBuf stage_aout[2];
+    int aslot = 0;
 
     size_t in_bytes() const { return kind_bytes(sk); }
     size_t out_bytes() const { return kind_bytes(csk); }
@@ -71,7 +78,23 @@ struct FirCore {
         os_state = nullptr;
         if (mx_state) fir_mx_release(mx_state);
         mx_state = nullptr;
+        if (d2h) (void)hipStreamSynchronize(d2h);
+        for (int i = 0; i < 2; ++i) {
+            stage_aout[i].release();
+            if (ev_k[i]) (void)hipEventDestroy(ev_k[i]);
+            if (ev_o[i]) (void)hipEventDestroy(ev_o[i]);
+            ev_k[i] = ev_o[i] = nullptr;
+            ev_o_live[i] = false;
+        }
+        if (d2h) (void)hipStreamDestroy(d2h);
+        d2h = nullptr;
         stream.destroy();
+    }
+    int sync_all() {
+        DeviceGuard g(device);
+        SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
+        if (d2h) SDRGPU_HIP_TRY(hipStreamSynchronize(d2h));
+        return SDRGPU_OK;
     }
 
     int reset_state() {
@@ -228,6 +251,54 @@ struct FirCore {
         return SDRGPU_OK;
     }
 
+    // Host pointers, asynchronous: H2D + FIR + D2H enqueued on the handle's stream, no
+    // wait.  With pinned buffers (sdrgpu_host_alloc) the copies are DMA straight from/to
+    // the caller's memory, so a caller that double-buffers fills block i+1 while block i is
+    // in flight -- the Block adapter's producer/consumer split (block.rs:105-207) with the
+    // GPU as the consumer.  Calls on one handle are stream-ordered, so the staging buffers
+    // are reused safely; `in` must stay untouched and `out` unread until *_sync.
+    int process_host_async(const void* in, size_t n_in, void* out, size_t out_cap,
+                           size_t* n_out_ret) {
+        const size_t n_out = out_len(n_in);
+        if (n_out_ret) *n_out_ret = n_out;
+        if (n_out > out_cap) return SDRGPU_ERR_OUTPUT_CAP;
+        if (n_in == 0) return SDRGPU_OK;
+        if (!in || (n_out && !out)) return SDRGPU_ERR_INVALID;
+        DeviceGuard g(device);
+        if (!g.ok()) return SDRGPU_ERR_DEVICE;
+        const size_t ib = in_bytes(), ob = out_bytes();
+        int st;
+        if (!d2h) {
+            SDRGPU_HIP_TRY(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+            for (int i = 0; i < 2; ++i) {
+                SDRGPU_HIP_TRY(hipEventCreateWithFlags(&ev_k[i], hipEventDisableTiming));
+                SDRGPU_HIP_TRY(hipEventCreateWithFlags(&ev_o[i], hipEventDisableTiming));
+            }
+        }
+        const int slot = aslot;
+        aslot ^= 1;
+        DevBuf& so = stage_aout[slot];
+        if (stage_in.cap < nch * n_in * ib || so.cap < nch * (n_out ? n_out : 1) * ob)
+            if ((st = sync_all())) return st;  // growing frees buffers that may be in flight
+        if ((st = stage_in.ensure(nch * n_in * ib))) return st;
+        if ((st = so.ensure(nch * (n_out ? n_out : 1) * ob))) return st;
+        SDRGPU_HIP_TRY(hipMemcpyAsync(stage_in.ptr, in, nch * n_in * ib, hipMemcpyHostToDevice,
+                                      stream.cur));
+        // the previous download from this slot must finish before the FIR overwrites it
+        if (ev_o_live[slot]) SDRGPU_HIP_TRY(hipStreamWaitEvent(stream.cur, ev_o[slot], 0));
+        size_t got = 0;
+        if ((st = run_dev(stage_in.ptr, n_in, n_in, so.ptr, n_out, &got))) return st;
+        if (n_out) {
+            SDRGPU_HIP_TRY(hipEventRecord(ev_k[slot], stream.cur));
+            SDRGPU_HIP_TRY(hipStreamWaitEvent(d2h, ev_k[slot], 0));
+            SDRGPU_HIP_TRY(hipMemcpyAsync(out, so.ptr, nch * n_out * ob, hipMemcpyDeviceToHost,
+                                          d2h));
+            SDRGPU_HIP_TRY(hipEventRecord(ev_o[slot], d2h));
+            ev_o_live[slot] = true;
+        }
+        return SDRGPU_OK;
+    }
+
     int clone_into(FirCore* dst) const {
         int st = dst->init(device, sk, tk, taps_host.data(), (size_t)K, (uint32_t)D, nch);
         if (st) return st;
@@ -306,6 +377,12 @@ int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out, si
     return h->core.process_host(in, n_in, n_in, out, out_cap, out_cap, n_out);
 }
 
+int sdrgpu_fir_process_async(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
+                             size_t out_cap, size_t* n_out) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    return h->core.process_host_async(in, n_in, out, out_cap, n_out);
+}
+
 int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d_out,
                            size_t out_cap, size_t* n_out) {
     if (!h) return SDRGPU_ERR_INVALID;
@@ -319,9 +396,7 @@ int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d
 
 int sdrgpu_fir_sync(sdrgpu_fir* h) {
     if (!h) return SDRGPU_ERR_INVALID;
-    DeviceGuard g(h->core.device);
-    SDRGPU_HIP_TRY(hipStreamSynchronize(h->core.stream.cur));
-    return SDRGPU_OK;
+    return h->core.sync_all();
 }
 
 int sdrgpu_fir_reset(sdrgpu_fir* h) {

@@ -73,6 +73,8 @@ SIGNATURES = [
     # device memory / events
     ("sdrgpu_dev_alloc", c_int, [c_int, c_size_t, _PH]),
     ("sdrgpu_dev_free", c_int, [c_int, c_void_p]),
+    ("sdrgpu_host_alloc", c_int, [c_int, c_size_t, _PH]),
+    ("sdrgpu_host_free", c_int, [c_void_p]),
     ("sdrgpu_dev_copy", c_int, [c_int, c_void_p, c_void_p, c_size_t, c_int]),
     ("sdrgpu_dev_memset", c_int, [c_int, c_void_p, c_int, c_size_t]),
     ("sdrgpu_dev_synchronize", c_int, [c_int]),
@@ -89,6 +91,7 @@ SIGNATURES = [
     ("sdrgpu_fir_output_len", c_int, [_H, c_size_t, _PS]),
     ("sdrgpu_fir_process", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_process_dev", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
+    ("sdrgpu_fir_process_async", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_sync", c_int, [_H]),
     ("sdrgpu_fir_reset", c_int, [_H]),
     ("sdrgpu_fir_clone", c_int, [_H, _PH]),

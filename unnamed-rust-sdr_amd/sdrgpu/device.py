@@ -75,6 +75,33 @@ class DeviceBuffer:
             pass
 
 
+class PinnedBuffer:
+    """Page-locked host memory (sdrgpu_host_alloc) viewed as a numpy array; the buffer type
+    the *_async entry points stream from/to without blocking."""
+
+    def __init__(self, n: int, dtype=np.complex64, device: int = 0):
+        self.dtype = np.dtype(dtype)
+        self.n = int(n)
+        p = ctypes.c_void_p()
+        check(lib().sdrgpu_host_alloc(device, max(1, self.n * self.dtype.itemsize),
+                                      ctypes.byref(p)), "sdrgpu_host_alloc")
+        self.ptr = p.value
+        buf = (ctypes.c_char * (self.n * self.dtype.itemsize)).from_address(self.ptr)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=self.n)
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            lib().sdrgpu_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Event:
     def __init__(self, device: int = 0):
         p = ctypes.c_void_p()

@@ -165,6 +165,14 @@ class FirFilter:
         y = self.process(np.asarray([value]))
         return y[0] if y.size else None
 
+    def process_async(self, in_ptr: int, n_in: int, out_ptr: int, out_cap: int) -> int:
+        """Host pointers (pinned: device.PinnedBuffer), enqueued without waiting; returns
+        n_out.  Read the output after sync()."""
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_fir_process_async(self._h, in_ptr, n_in, out_ptr, out_cap,
+                                             ctypes.byref(got)), "sdrgpu_fir_process_async")
+        return got.value
+
     def process_dev(self, d_in_ptr: int, n_in: int, d_out_ptr: int, out_cap: int) -> int:
         """Enqueue on the handle's stream with device pointers; returns n_out."""
         got = ctypes.c_size_t()
