@@ -380,6 +380,11 @@ struct FftPlanDev {
     float norm = 1.f;
     float2* tw4096 = nullptr;
     float2* twM = nullptr;
+    // 64K four-step, two-stream mode: batches alternate between the caller's stream and
+    // `aux` (each with its own half of the scratch slab) so one batch's pass B overlaps the
+    // next batch's pass A instead of draining the GPU at every pass boundary
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 void* fft_plan_create(int M, int* status) {
@@ -425,6 +430,10 @@ void fft_plan_destroy(void* plan) {
     if (!p) return;
     if (p->tw4096) (void)hipFree(p->tw4096);
     if (p->twM) (void)hipFree(p->twM);
+    if (p->aux) (void)hipStreamSynchronize(p->aux);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->aux) (void)hipStreamDestroy(p->aux);
     delete p;
 }
 
@@ -499,13 +508,33 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
             const char* e = getenv("SDRGPU_FFT64K_NT");
             return !e || atoi(e) != 0;
         }();
+        static const int nstreams = [] {
+            const char* e = getenv("SDRGPU_FFT64K_STREAMS");  // default 2 (2.63-2.70 vs 2.77-2.79 ms)
+            return e && atoi(e) == 1 ? 1 : 2;
+        }();
+        const bool two = nstreams == 2 && scratch_frames >= 2 && fr.nframes > (long)scratch_frames / 2;
+        if (two && !p->aux) {
+            if (hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess)
+                return SDRGPU_ERR_DEVICE;
+        }
+        const long batch = two ? (long)scratch_frames / 2 : (long)scratch_frames;
+        if (two) {  // aux starts after everything already queued on s
+            if (hipEventRecord(p->ev_fork, s) != hipSuccess ||
+                hipStreamWaitEvent(p->aux, p->ev_fork, 0) != hipSuccess)
+                return SDRGPU_ERR_DEVICE;
+        }
         F64Args a{};
         a.tw = p->tw4096;
         a.twM = p->twM;
         a.norm = p->norm;
-        a.scratch = scratch;
-        for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
-            const long nf = std::min((long)scratch_frames, fr.nframes - f0);
+        long bi = 0;
+        for (long f0 = 0; f0 < fr.nframes; f0 += batch, ++bi) {
+            const long nf = std::min(batch, fr.nframes - f0);
+            const bool odd = two && (bi & 1);
+            hipStream_t st = odd ? p->aux : s;
+            a.scratch = scratch + (odd ? batch * (long)p->M : 0L);
             a.src = src;
             if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
             else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
@@ -513,23 +542,28 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
             a.out = out + f0 * (long)p->M;
             const dim3 g((unsigned)(nf * (256 / cb))), b(16 * cb);
             if (cb == 64 && nt) {
-                hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, st, a);
                 SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<64, true>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_b<64, true>), g, b, 0, st, a);
             } else if (cb == 64) {
-                hipLaunchKernelGGL((fft64k_pass_a<64, false>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_a<64, false>), g, b, 0, st, a);
                 SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<64, false>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_b<64, false>), g, b, 0, st, a);
             } else if (nt) {
-                hipLaunchKernelGGL((fft64k_pass_a<32, true>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_a<32, true>), g, b, 0, st, a);
                 SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<32, true>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_b<32, true>), g, b, 0, st, a);
             } else {
-                hipLaunchKernelGGL((fft64k_pass_a<32, false>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_a<32, false>), g, b, 0, st, a);
                 SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<32, false>), g, b, 0, s, a);
+                hipLaunchKernelGGL((fft64k_pass_b<32, false>), g, b, 0, st, a);
             }
             SDRGPU_LAUNCH_CHECK();
+        }
+        if (two) {  // s continues only after aux's batches
+            if (hipEventRecord(p->ev_join, p->aux) != hipSuccess ||
+                hipStreamWaitEvent(s, p->ev_join, 0) != hipSuccess)
+                return SDRGPU_ERR_DEVICE;
         }
         return SDRGPU_OK;
     }
