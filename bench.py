@@ -129,6 +129,9 @@ def main():
     from sdrgpu import _lib
     from sdrgpu.device import DeviceBuffer, Event, synchronize
 
+    # one GPU per rank; ranks beyond the visible GPUs share them round-robin (a rehearsal
+    # of the N-rank path on a smaller box -- on a full node local < device_count)
+    local = local % max(1, sdrgpu.device_count())
     taps = ss.firwin(255, 0.2).astype(np.float32)
     n = 1 << args.log2n
     D = 4
