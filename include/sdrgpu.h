@@ -235,6 +235,14 @@ typedef struct {
 typedef struct sdrgpu_pll sdrgpu_pll;
 
 int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu_pll** out);
+/* What `out` receives (the lock mask is unchanged):
+ *   SDRGPU_PLL_OUT_FILTER (default): output filter of phasedif * rate, 0.0 when unlocked
+ *     (Pll::apply, pll.rs:79-84; None -> 0.0 as src/main.rs:49);
+ *   SDRGPU_PLL_OUT_STEREO_DIFF: the FM stereo pilot map of src/main.rs:58-66 -- the input is
+ *     Complex::new(v, 0.0) and out = (v / value.powi(2)).re * 0.5 with the PLL's updated NCO
+ *     value when locked, else 0.0 (mono = v * 0.5 stays on the caller). */
+enum sdrgpu_pll_output { SDRGPU_PLL_OUT_FILTER = 0, SDRGPU_PLL_OUT_STEREO_DIFF = 1 };
+int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode);
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
 int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** hip_stream);
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,

@@ -307,6 +307,28 @@ static inline float pll_apply(pll_state* s, c32 x, uint8_t* locked_out, int loop
     return 0.0f;                                               /* main.rs:49 */
 }
 
+/* src/main.rs:56-69: the stereo pilot map over a real stream v (one channel):
+ * mono = v * 0.5; diff = Some -> (v / value.powi(2)).re * 0.5, None -> 0.0, where
+ * pllpilot.apply(Complex::new(v, 0.0)) updated `value`.  num-complex 0.2: powi(2) =
+ * value * value; f32 / Complex -> re = v * w.re / w.norm_sqr(). */
+void oracle_pll_stereo(const oracle_pll_params* p, const float* v, size_t n, float* mono,
+                       float* diff, uint8_t* locked) {
+    pll_state s; pll_design(p, &s);
+    const int loop_ident = p->loopf.kind == ORACLE_BQ_IDENTITY;
+    for (size_t i = 0; i < n; ++i) {
+        c32 x = {v[i], 0.0f};
+        (void)pll_apply(&s, x, &locked[i], loop_ident);
+        mono[i] = v[i] * 0.5f;
+        if (locked[i]) {
+            c32 w = cmul(s.value, s.value);
+            float nrm = w.re * w.re + w.im * w.im;
+            diff[i] = v[i] * w.re / nrm * 0.5f;
+        } else {
+            diff[i] = 0.0f;
+        }
+    }
+}
+
 typedef struct {
     const oracle_pll_params* p; const float* in; size_t ld_in, n; float* out;
     uint8_t* locked; size_t ld_out; size_t ch0, ch1;

@@ -78,6 +78,10 @@ void oracle_pll_batch(const oracle_pll_params* p, size_t nch, const float* in,
                       size_t ld_in, size_t n, float* out, uint8_t* locked,
                       size_t ld_out, int nthreads);
 
+/* FM stereo pilot map (src/main.rs:56-69) on one real stream: mono, diff, lock mask. */
+void oracle_pll_stereo(const oracle_pll_params* p, const float* v, size_t n, float* mono,
+                       float* diff, uint8_t* locked);
+
 /* ---------------- FFT (src/fft.rs:3-37) ------------------------------------------ */
 /* fft::fft on one frame of n complex samples: forward DFT (computed in float64,
  * rounded to f32 -- rustfft 3.0 itself is unpinned), fftshift-collated,

@@ -55,6 +55,8 @@ def lib():
                                         c_void_p]
         L.oracle_pll_batch.argtypes = [POINTER(PllParams), c_size_t, c_void_p, c_size_t,
                                        c_size_t, c_void_p, c_void_p, c_size_t, c_int]
+        L.oracle_pll_stereo.argtypes = [POINTER(PllParams), c_void_p, c_size_t, c_void_p,
+                                         c_void_p, c_void_p]
         L.oracle_fft_frame.argtypes = [c_void_p, c_size_t, c_void_p]
         L.oracle_stft.restype = c_size_t
         L.oracle_stft.argtypes = [c_void_p, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t,
@@ -153,6 +155,15 @@ def pll_batch(params, x, nthreads=1):
     lib().oracle_pll_batch(ctypes.byref(params), nch, x.ctypes.data, n, n, out.ctypes.data,
                            locked.ctypes.data, n, nthreads)
     return out, locked
+
+
+def pll_stereo(params, v):
+    v = np.ascontiguousarray(v, np.float32)
+    mono, diff = np.empty_like(v), np.empty_like(v)
+    locked = np.empty(v.size, np.uint8)
+    lib().oracle_pll_stereo(ctypes.byref(params), v.ctypes.data, v.size, mono.ctypes.data,
+                            diff.ctypes.data, locked.ctypes.data)
+    return mono, diff, locked
 
 
 def fft_frame(x):

@@ -123,3 +123,36 @@ def test_pll_tone_kat(sdr):
 def test_pll_apply_single_sample(sdr):
     pll = main_rs_design(sdr).design(RATE)
     assert pll.apply(1 + 0j) is None  # value starts at 0+0i -> c = 0 -> not locked
+
+
+def test_pll_stereo_pilot_chain(sdr, oracle):
+    """src/main.rs:56-69: 19 kHz pilot PLL on the 144 kHz FM audio, mono = v/2 and
+    diff = (v / value.powi(2)).re / 2 while the pilot is locked -- bit-exact, batched."""
+    f = sdr.filter
+    rate = 144000.0
+    rng = np.random.default_rng(19)
+    nch, n = 6, 60000
+    t = np.arange(n) / rate
+    v = np.empty((nch, n), np.float32)
+    for c in range(nch):
+        lr = 0.3 * np.sin(2 * np.pi * 440 * t)
+        lmr = 0.2 * np.sin(2 * np.pi * 1000 * t + c)
+        ph = rng.uniform(-1.2, 1.2) if c < 4 else rng.uniform(2.0, 4.0)
+        v[c] = (lr + 0.2 * np.cos(2 * np.pi * 19000 * t + ph)
+                + lmr * np.cos(2 * np.pi * 38000 * t + 2 * ph)
+                + 0.01 * rng.standard_normal(n)).astype(np.float32)
+    design = f.PllDesign(19000.0, 0.0002, f.BiquadD.LowPass(200.0, 0.7),
+                         f.BiquadD.LowPass(20.0, 0.7), f.BiquadD.LowPass(20.0, 0.7))
+    pll = design.design(rate, nch=nch)
+    mono, diff, locked = pll.stereo(v)
+    op = oracle.pll_params(19000.0, 0.0002, rate, (1, 200.0, 0.7), (1, 20.0, 0.7),
+                           (1, 20.0, 0.7))
+    for c in range(nch):
+        om, od, ol = oracle.pll_stereo(op, v[c])
+        assert np.array_equal(mono[c], om)
+        assert np.array_equal(locked[c], ol), c
+        assert np.array_equal(diff[c], od), c
+    assert locked.any() and diff[locked.astype(bool)].std() > 0
+    # the normal output mode is restored afterwards and state carried on
+    out2, _ = pll.process(v[:, :100].astype(np.complex64))
+    assert out2.shape == (nch, 100)

@@ -128,6 +128,13 @@ int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu
     return SDRGPU_OK;
 }
 
+int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode) {
+    if (!h || mode < SDRGPU_PLL_OUT_FILTER || mode > SDRGPU_PLL_OUT_STEREO_DIFF)
+        return SDRGPU_ERR_INVALID;
+    h->dp.out_mode = mode;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* s) {
     if (!h) return SDRGPU_ERR_INVALID;
     h->stream.set(s);
@@ -203,6 +210,7 @@ int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {
     if (!h || !out) return SDRGPU_ERR_INVALID;
     int st = sdrgpu_pll_create(h->device, &h->params, (size_t)h->dp.nch, out);
     if (st) return st;
+    (*out)->dp.out_mode = h->dp.out_mode;
     DeviceGuard g(h->device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
     SDRGPU_HIP_TRY(hipMemcpy((*out)->d_state, h->d_state, h->dp.nch * sizeof(PllChannelState),

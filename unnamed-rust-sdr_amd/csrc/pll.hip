@@ -5,6 +5,7 @@
 //   c = x * conj(v);  phasedif = arg(loop(c)) * gain;  nphase = fract(nphase + ref + phasedif)
 //   v = from_polar(1, 2 pi nphase);  locked = lock(c.re);  out = output(phasedif * rate)
 //   -> Some(out) if locked > 0.01 else None   (None written as 0.0, src/main.rs:49)
+// out_mode 1 writes the stereo difference signal of src/main.rs:58-66 instead of `out`.
 //
 // The recurrence is serial and nonlinear (atan2 -> NCO -> sin/cos each sample), so it is
 // latency-bound, not HBM- or FLOP-bound; the next 8 samples of every lane
@@ -97,6 +98,18 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
         const float o = p.out_ident ? phasedif * p.rate
                                     : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
         const bool lockd = lockv > 0.01f;                          // :80
+        if (p.out_mode == 1) {
+            // src/main.rs:58-66, the stereo pilot: input = Complex::new(v, 0.0);
+            // diff = (v / value.powi(2)).re * 0.5 when locked.  powi(2) = value * value
+            // (num-complex Mul); f32 / Complex: re = v * w.re / norm_sqr(w)
+            const float wr = s.vr * s.vr - s.vi * s.vi;
+            const float wi = s.vr * s.vi + s.vi * s.vr;
+            const float nrm = wr * wr + wi * wi;
+            const float dre = v.x * wr / nrm;
+            ov = lockd ? dre * 0.5f : 0.0f;
+            lv = lockd ? 1 : 0;
+            return;
+        }
         ov = lockd ? o : 0.0f;
         lv = lockd ? 1 : 0;
     };

@@ -12,6 +12,7 @@ struct PllDevParams {
     float gain;       // pll.rs:52
     float loopc[5], outc[5], lockc[5];  // b0 b1 b2 na1 na2 (biquad.rs:25-38)
     int loop_ident, out_ident, lock_ident;
+    int out_mode;     // SDRGPU_PLL_OUT_FILTER (0) or SDRGPU_PLL_OUT_STEREO_DIFF (1)
 };
 
 // Per-channel state (Pll fields nphase/value + three biquad states), 20 floats.

@@ -30,6 +30,9 @@ FIR_DIRECT = 1
 FIR_OVERLAP_SAVE = 2
 FIR_MATRIX = 3
 
+PLL_OUT_FILTER = 0
+PLL_OUT_STEREO_DIFF = 1
+
 BQ_IDENTITY = 0
 BQ_LOWPASS = 1
 BQ_HIGHPASS = 2
@@ -133,6 +136,7 @@ SIGNATURES = [
     ("sdrgpu_stft_destroy", None, [_H]),
     # PLL
     ("sdrgpu_pll_create", c_int, [c_int, POINTER(PllParamsC), c_size_t, _PH]),
+    ("sdrgpu_pll_set_output_mode", c_int, [_H, c_int]),
     ("sdrgpu_pll_set_stream", c_int, [_H, c_void_p]),
     ("sdrgpu_pll_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_pll_process", c_int,

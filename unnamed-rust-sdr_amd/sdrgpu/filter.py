@@ -452,6 +452,22 @@ class Pll:
     def reset(self):
         check(lib().sdrgpu_pll_reset(self._h), "sdrgpu_pll_reset")
 
+    def set_output_mode(self, mode: int):
+        """_lib.PLL_OUT_FILTER (Pll::apply's output) or _lib.PLL_OUT_STEREO_DIFF."""
+        check(lib().sdrgpu_pll_set_output_mode(self._h, mode), "sdrgpu_pll_set_output_mode")
+
+    def stereo(self, v):
+        """src/main.rs:56-69 with this PLL as `pllpilot`: real audio v (nch, n) or (n,) ->
+        (mono, diff, locked); mono = v * 0.5, diff = (v / value.powi(2)).re * 0.5 when the
+        pilot is locked else 0.0."""
+        v = np.ascontiguousarray(v, np.float32)
+        self.set_output_mode(_lib.PLL_OUT_STEREO_DIFF)
+        try:
+            diff, locked = self.process(v.astype(np.complex64))  # Complex::new(v, 0.0)
+        finally:
+            self.set_output_mode(_lib.PLL_OUT_FILTER)
+        return v * np.float32(0.5), diff, locked
+
     def set_stream(self, stream_ptr):
         check(lib().sdrgpu_pll_set_stream(self._h, stream_ptr), "sdrgpu_pll_set_stream")
 
