@@ -243,6 +243,10 @@ int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu
  *     value when locked, else 0.0 (mono = v * 0.5 stays on the caller). */
 enum sdrgpu_pll_output { SDRGPU_PLL_OUT_FILTER = 0, SDRGPU_PLL_OUT_STEREO_DIFF = 1 };
 int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode);
+/* Input samples: SDRGPU_C64 (default) or SDRGPU_CU8 -- raw rtl_tcp I/Q byte pairs
+ * (src/main.rs:48-49 feeds rtl.listen() straight into the PLL), converted in the load as
+ * RtlTcpSignal::next does, (v - 128) / 128 (src/rtltcp.rs:156-164); ld_in counts samples. */
+int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind);
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
 int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** hip_stream);
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,

@@ -156,3 +156,22 @@ def test_pll_stereo_pilot_chain(sdr, oracle):
     # the normal output mode is restored afterwards and state carried on
     out2, _ = pll.process(v[:, :100].astype(np.complex64))
     assert out2.shape == (nch, 100)
+
+
+def test_pll_rtl_tcp_u8_input(sdr, oracle):
+    """src/main.rs:48-49: rtl.listen() feeds the PLL directly; u8 I/Q converted in the load
+    ((v - 128) / 128, src/rtltcp.rs:156-164) gives exactly the C64 path's outputs."""
+    rng = np.random.default_rng(23)
+    nch, n = 70, 9001
+    x = fm_channels(rng, nch, n)
+    iq = np.empty((nch, 2 * n), np.uint8)
+    iq[:, 0::2] = np.clip(np.round(x.real * 100 + 128), 0, 255)
+    iq[:, 1::2] = np.clip(np.round(x.imag * 100 + 128), 0, 255)
+    xc = oracle.u8_to_c64(iq.reshape(-1)).reshape(nch, n)
+    d = main_rs_design(sdr)
+    a = d.design(RATE, nch=nch)
+    out_u8, lk_u8 = a.process_u8(iq[:, :4000])
+    o2, l2 = a.process_u8(iq[:, 4000:])
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), xc)
+    assert np.array_equal(np.concatenate([out_u8, o2], 1), ref_out)
+    assert np.array_equal(np.concatenate([lk_u8, l2], 1), ref_lk)

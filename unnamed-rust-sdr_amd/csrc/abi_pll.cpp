@@ -128,6 +128,12 @@ int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu
     return SDRGPU_OK;
 }
 
+int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind) {
+    if (!h || (sample_kind != SDRGPU_C64 && sample_kind != SDRGPU_CU8)) return SDRGPU_ERR_INVALID;
+    h->dp.in_u8 = sample_kind == SDRGPU_CU8;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode) {
     if (!h || mode < SDRGPU_PLL_OUT_FILTER || mode > SDRGPU_PLL_OUT_STEREO_DIFF)
         return SDRGPU_ERR_INVALID;
@@ -154,7 +160,7 @@ int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t
     if (!d_in || !d_out || !d_locked || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
-    return pll_launch(h->dp, static_cast<const float2*>(d_in), (long)ld_in, (long)n, d_out, d_locked,
+    return pll_launch(h->dp, d_in, (long)ld_in, (long)n, d_out, d_locked,
                       (long)ld_out, h->d_state, h->stream.cur);
 }
 
@@ -167,13 +173,14 @@ int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, fl
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
     const size_t nch = (size_t)h->dp.nch;
     int st;
-    if ((st = h->stage_in.ensure(nch * n * sizeof(float2))) ||
+    const size_t sb = h->dp.in_u8 ? 2 : sizeof(float2);  // bytes per input sample
+    if ((st = h->stage_in.ensure(nch * n * sb)) ||
         (st = h->stage_out.ensure(nch * n * sizeof(float))) ||
         (st = h->stage_lock.ensure(nch * n)))
         return st;
-    SDRGPU_HIP_TRY(hipMemcpy2DAsync(h->stage_in.ptr, n * sizeof(float2), in, ld_in * sizeof(float2),
-                                    n * sizeof(float2), nch, hipMemcpyHostToDevice, h->stream.cur));
-    if ((st = pll_launch(h->dp, static_cast<const float2*>(h->stage_in.ptr), (long)n, (long)n,
+    SDRGPU_HIP_TRY(hipMemcpy2DAsync(h->stage_in.ptr, n * sb, in, ld_in * sb, n * sb, nch,
+                                    hipMemcpyHostToDevice, h->stream.cur));
+    if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n,
                          static_cast<float*>(h->stage_out.ptr), static_cast<uint8_t*>(h->stage_lock.ptr),
                          (long)n, h->d_state, h->stream.cur)))
         return st;
@@ -211,6 +218,7 @@ int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {
     int st = sdrgpu_pll_create(h->device, &h->params, (size_t)h->dp.nch, out);
     if (st) return st;
     (*out)->dp.out_mode = h->dp.out_mode;
+    (*out)->dp.in_u8 = h->dp.in_u8;
     DeviceGuard g(h->device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
     SDRGPU_HIP_TRY(hipMemcpy((*out)->d_state, h->d_state, h->dp.nch * sizeof(PllChannelState),

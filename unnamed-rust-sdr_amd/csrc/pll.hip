@@ -50,14 +50,27 @@ __device__ __forceinline__ float bq_real(const Bq& c, float x, float& x1, float&
     return out;
 }
 
-__global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const float2* __restrict__ in,
+// U8: samples are rtl_tcp byte pairs, converted as RtlTcpSignal::next does
+// ((v as f32 - 128.0) / 128.0, src/rtltcp.rs:156-164 -- exact in f32) inside the load
+template <bool U8>
+__global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const void* __restrict__ in_,
                                                         long ld_in, long n, float* __restrict__ out,
                                                         uint8_t* __restrict__ locked, long ld_out,
                                                         PllChannelState* __restrict__ state) {
     const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
     if (ch >= p.nch) return;
     PllChannelState s = state[ch];
-    const float2* __restrict__ x = in + ch * ld_in;
+    const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;
+    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;
+    auto ld = [&](long i) -> float2 {
+        if constexpr (U8) {
+            const unsigned w = xu[i];
+            return make_float2(((float)(w & 255u) - 128.0f) / 128.0f,
+                               ((float)(w >> 8) - 128.0f) / 128.0f);
+        } else {
+            return xf[i];
+        }
+    };
     float* __restrict__ y = out + ch * ld_out;
     uint8_t* __restrict__ lk = locked + ch * ld_out;
     const Bq L = {p.loopc[0], p.loopc[1], p.loopc[2], p.loopc[3], p.loopc[4]};
@@ -119,7 +132,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
     float2 buf[kChunk];
     if (nfull > 0) {
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) buf[k] = x[k];
+        for (int k = 0; k < kChunk; ++k) buf[k] = ld(k);
     }
     for (long i = 0; i < nfull; i += kChunk) {
         float2 cur[kChunk];
@@ -127,7 +140,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
         for (int k = 0; k < kChunk; ++k) cur[k] = buf[k];
         if (i + kChunk < nfull) {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) buf[k] = x[i + kChunk + k];  // prefetch
+            for (int k = 0; k < kChunk; ++k) buf[k] = ld(i + kChunk + k);  // prefetch
         }
         float ov[kChunk];
         uint8_t lv[kChunk];
@@ -143,7 +156,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
     for (long i = nfull; i < n; ++i) {
         float o;
         uint8_t l;
-        step(x[i], o, l);
+        step(ld(i), o, l);
         y[i] = o;
         lk[i] = l;
     }
@@ -152,12 +165,16 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const fl
 
 }  // namespace
 
-int pll_launch(const PllDevParams& p, const float2* in, long ld_in, long n, float* out,
+int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
     if (n <= 0) return SDRGPU_OK;
     const long nblk = (p.nch + kPllBlock - 1) / kPllBlock;
-    hipLaunchKernelGGL(pll_kernel, dim3((unsigned)nblk), dim3(kPllBlock), 0, s, p, in, ld_in, n, out,
-                       locked, ld_out, state);
+    if (p.in_u8)
+        hipLaunchKernelGGL(pll_kernel<true>, dim3((unsigned)nblk), dim3(kPllBlock), 0, s, p, in,
+                           ld_in, n, out, locked, ld_out, state);
+    else
+        hipLaunchKernelGGL(pll_kernel<false>, dim3((unsigned)nblk), dim3(kPllBlock), 0, s, p, in,
+                           ld_in, n, out, locked, ld_out, state);
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }

@@ -13,6 +13,7 @@ struct PllDevParams {
     float loopc[5], outc[5], lockc[5];  // b0 b1 b2 na1 na2 (biquad.rs:25-38)
     int loop_ident, out_ident, lock_ident;
     int out_mode;     // SDRGPU_PLL_OUT_FILTER (0) or SDRGPU_PLL_OUT_STEREO_DIFF (1)
+    int in_u8;        // input = rtl_tcp interleaved u8 I/Q (2 B/sample), (v - 128) / 128
 };
 
 // Per-channel state (Pll fields nphase/value + three biquad states), 20 floats.
@@ -24,7 +25,7 @@ struct PllChannelState {
     float pad;
 };
 
-int pll_launch(const PllDevParams& p, const float2* in, long ld_in, long n, float* out,
+int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s);
 
 }  // namespace sdrgpu

@@ -137,6 +137,7 @@ SIGNATURES = [
     # PLL
     ("sdrgpu_pll_create", c_int, [c_int, POINTER(PllParamsC), c_size_t, _PH]),
     ("sdrgpu_pll_set_output_mode", c_int, [_H, c_int]),
+    ("sdrgpu_pll_set_input_kind", c_int, [_H, c_int]),
     ("sdrgpu_pll_set_stream", c_int, [_H, c_void_p]),
     ("sdrgpu_pll_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_pll_process", c_int,

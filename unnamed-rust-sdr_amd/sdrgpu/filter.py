@@ -476,6 +476,24 @@ class Pll:
         check(lib().sdrgpu_pll_get_stream(self._h, ctypes.byref(s)), "sdrgpu_pll_get_stream")
         return s.value or 0
 
+    def process_u8(self, iq):
+        """rtl_tcp bytes: iq (nch, 2n) or (2n,) uint8 interleaved I/Q -> (out, locked)."""
+        iq = np.ascontiguousarray(iq, dtype=np.uint8)
+        squeeze = iq.ndim == 1
+        if squeeze:
+            iq = iq[None, :]
+        n = iq.shape[1] // 2
+        out = np.empty((self.nch, max(n, 1)), dtype=np.float32)
+        locked = np.empty((self.nch, max(n, 1)), dtype=np.uint8)
+        check(lib().sdrgpu_pll_set_input_kind(self._h, CU8), "sdrgpu_pll_set_input_kind")
+        try:
+            check(lib().sdrgpu_pll_process(self._h, iq.ctypes.data, n, n, out.ctypes.data,
+                                           locked.ctypes.data, out.shape[1]), "sdrgpu_pll_process")
+        finally:
+            check(lib().sdrgpu_pll_set_input_kind(self._h, C64), "sdrgpu_pll_set_input_kind")
+        out, locked = out[:, :n], locked[:, :n]
+        return (out[0], locked[0]) if squeeze else (out, locked)
+
     def process(self, x):
         """x: (nch, n) or (n,) complex -> (out float32, locked uint8) of the same shape."""
         x = np.ascontiguousarray(x, dtype=np.complex64)
