@@ -7,8 +7,8 @@ without the built library raises ImportError.
 """
 from . import _lib
 from ._lib import C64, CU8, F32, SdrGpuError, device_count, lib
-from . import device, fft, filter, resample, shard, signal  # noqa: F401
+from . import device, fft, filter, resample, rtltcp, shard, signal  # noqa: F401
 
 lib()  # fail loudly at import if the HIP library is missing
 
-__all__ = ["device", "fft", "filter", "resample", "shard", "signal", "C64", "CU8", "F32", "SdrGpuError", "device_count", "lib"]
+__all__ = ["device", "fft", "filter", "resample", "rtltcp", "shard", "signal", "C64", "CU8", "F32", "SdrGpuError", "device_count", "lib"]

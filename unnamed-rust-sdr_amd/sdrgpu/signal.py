@@ -89,7 +89,10 @@ class Signal:
         def gen():
             p = design.design(up.rate())
             for b in up.blocks():
-                out, locked = p.process(np.asarray(b, np.complex64))
+                if up.sample_kind == _lib.CU8:  # rtl_tcp bytes straight into the PLL
+                    out, locked = p.process_u8(b)
+                else:
+                    out, locked = p.process(np.asarray(b, np.complex64))
                 yield np.rec.fromarrays([out, locked.astype(bool)], names="value,locked")
         return Signal(self._rate, gen, None)
 
