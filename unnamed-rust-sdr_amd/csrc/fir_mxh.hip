@@ -76,6 +76,7 @@ struct MxhParams {
     float2* out;
     long ld_out;
     long tpc, spc, seg_tiles, units;
+    long rot;  // per-unit start rotation stride in tiles (0 = off)
     int vec_out;
 };
 
@@ -263,9 +264,16 @@ void fir_mxh_kernel(MxhParams p) {
                            : base + 4 * lane;
 
     for (long u = wave; u < p.units; u += nwaves) {
-        const long ch = u / p.spc;
-        const long t0 = (u - ch * p.spc) * p.seg_tiles;
-        const long nt = std::min(p.seg_tiles, p.tpc - t0);
+      const long ch = u / p.spc;
+      const long tu = (u - ch * p.spc) * p.seg_tiles;
+      const long ntu = std::min(p.seg_tiles, p.tpc - tu);
+      if (ntu <= 0) continue;
+      // rot > 0: start the unit's tiles at a unit-dependent offset and wrap, so that the
+      // waves' stream positions are not all congruent modulo the (power-of-two) unit size
+      const long rot = p.rot > 0 && ntu > 1 ? (u * p.rot) % ntu : 0;
+      for (int part = 0; part < (rot ? 2 : 1); ++part) {
+        const long t0 = part == 0 ? tu + rot : tu;
+        const long nt = part == 0 ? ntu - rot : rot;
         if (nt <= 0) continue;
         const float2* __restrict__ in = p.in + ch * p.ld_in;
         const unsigned* __restrict__ in4 = p.in_u8 + ch * (p.ld_in / 2);  // U8: dword = 2 samples
@@ -499,6 +507,7 @@ void fir_mxh_kernel(MxhParams p) {
                  ...);
             }(std::make_integer_sequence<int, U>());
         }
+      }
     }
 
     if (p.hist_next) {  // stream history carry, spread over the whole grid
@@ -590,6 +599,11 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     if (seg_env > 0) p.seg_tiles = std::min(p.seg_tiles, seg_env);
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
+    static const long rot_env = [] {
+        const char* e = getenv("SDRGPU_MXH_ROT");
+        return e ? atol(e) : 0L;
+    }();
+    p.rot = rot_env;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
     static const char* abl_env = getenv("SDRGPU_MX_ABLATION");
     const int abl = abl_env ? atoi(abl_env) : 0;
