@@ -841,7 +841,6 @@ __global__ __launch_bounds__(kOsBlock, 2) void fir_os5_kernel(OsParams p, long n
 #pragma unroll
         for (int j2 = 0; j2 < 4; ++j2) H[b][j2] = p.H[b * L + t + 256 * j2];
 
-    const long hop = (long)p.M * D;
     const long nquad = (nblk + 3) / 4;
     float2 v[16];
     long quad = blockIdx.x;
