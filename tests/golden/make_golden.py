@@ -12,7 +12,11 @@ Inputs are seeded; each fixture is a small .npz (no pickles).
   biquad.npz      RBJ designs (biquad.rs:83-155) in float64 + impulse responses
   fft.npz         fft::fft (fft.rs:3-28) of random frames, fftshift / sqrt(N)
   stft.npz        Window+Decimate framing (adapters/mod.rs:270-303) + fft per frame
+  resample.npz    libsamplerate ZOH / linear (src/resample.rs) from the closed form with
+                  exact rational positions q_k = k / ratio - 1 (x[-1] = x[0] after reset),
+                  not the serial f64 walk the oracle restates
 """
+from fractions import Fraction
 import os
 
 import numpy as np
@@ -93,6 +97,44 @@ def main():
                 fr[i] = xs[beg + i]
         Y[j] = np.fft.fftshift(np.fft.fft(fr)) / np.sqrt(N)
     np.savez(os.path.join(HERE, "stft.npz"), x=xs, n=N, hop=hop, y=Y)
+
+    # resampler: ratios of src/main.rs (1.8 Msps -> 144 kHz -> 48 kHz) and generic ones
+    cases = {}
+    for ci, (ratio, ch) in enumerate([(144000 / 1.8e6, 1), (48000 / 144000, 2), (1.37, 1),
+                                      (3.0, 2), (48000 / 44100, 1)]):
+        xr = rng.standard_normal((2000, ch)).astype(np.float32)
+        cases[f"x{ci}"] = xr
+        cases[f"ratio{ci}"] = np.float64(ratio)
+        cases[f"lin{ci}"], cases[f"linamb{ci}"] = src_closed_form(xr, ratio, True)
+        cases[f"zoh{ci}"], cases[f"zohamb{ci}"] = src_closed_form(xr, ratio, False)
+    np.savez(os.path.join(HERE, "resample.npz"), ncases=5, **cases)
+
+
+def src_closed_form(x, ratio, linear):
+    """One src_process call after reset at constant ratio, whole input, unlimited output:
+    output k sits at exact position q = k * inc - 1 (inc = the f64 1/ratio) between frames
+    floor(q) and floor(q)+1, frame -1 being last_value = x[0]; linear needs the right frame
+    (q < N - 1), ZOH holds the left one (q <= N - 1)."""
+    n = x.shape[0]
+    inc = Fraction(1.0 / ratio)
+    out, amb = [], []
+    k = 0
+    while True:
+        q = k * inc - 1
+        fl = q.numerator // q.denominator
+        if (linear and not q < n - 1) or (not linear and not q <= n - 1):
+            break
+        fr = float(q - fl)
+        amb.append(min(fr, 1 - fr) < 1e-9)  # the serial f64 walk may land on either side
+        a = x[max(fl, 0)].astype(np.float64)
+        if linear:
+            b = x[fl + 1].astype(np.float64)
+            f = float(q - fl)
+            out.append((a + f * (b - a)).astype(np.float32))
+        else:
+            out.append(a.astype(np.float32))
+        k += 1
+    return np.array(out, np.float32).reshape(-1, x.shape[1]), np.array(amb, bool)
 
 
 if __name__ == "__main__":

@@ -214,3 +214,25 @@ def test_signal_resample_with_matches_adapter(sdr, oracle):
     assert np.array_equal(y, np.concatenate(ref))
     with pytest.raises(resample.Error):
         signal.from_array(1.8e6, x).resample(48000.0).collect()
+
+
+def test_oracle_resample_golden(oracle):
+    """Oracle (serial f64 walk, libsamplerate's form) vs the closed form with exact rational
+    positions (tests/golden/make_golden.py): same outputs except where an output's position
+    is within 1e-9 of a frame boundary (the walk's rounding may land on either side: ZOH
+    then holds the other frame; linear moves by < 1e-5), same counts up to that boundary."""
+    import os
+    from conftest import ROOT
+    d = np.load(os.path.join(ROOT, "tests", "golden", "resample.npz"))
+    for i in range(int(d["ncases"])):
+        x, ratio = d[f"x{i}"], float(d[f"ratio{i}"])
+        for conv, key in ((LINEAR, "lin"), (ZOH, "zoh")):
+            used, y = oracle.SampleRate(conv, x.shape[1]).process(ratio, x, 100000)
+            ref, amb = d[f"{key}{i}"], d[f"{key}amb{i}"]
+            assert abs(len(y) - len(ref)) <= 1 and used >= x.shape[0] - 1, (i, key)
+            m = min(len(y), len(ref))
+            ok = ~amb[:m]
+            if conv == LINEAR:
+                assert np.abs(y[:m] - ref[:m]).max() <= 1e-5, (i, key)
+            else:
+                assert np.array_equal(y[:m][ok], ref[:m][ok]), (i, key)
