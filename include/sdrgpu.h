@@ -139,6 +139,10 @@ int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d
 int sdrgpu_fir_process_async(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
                              size_t out_cap, size_t* n_out);
 int sdrgpu_fir_sync(sdrgpu_fir* h);
+/* The algorithm (SDRGPU_FIR_DIRECT / _OVERLAP_SAVE / _MATRIX) that ran the most recent
+ * non-empty block; SDRGPU_FIR_AUTO before the first one.  Introspection for tests and
+ * benches (which kernel family a shape actually took); no reference counterpart. */
+int sdrgpu_fir_last_algorithm(const sdrgpu_fir* h, int* algo);
 int sdrgpu_fir_reset(sdrgpu_fir* h);                           /* FilterDesign::design -> fresh state */
 int sdrgpu_fir_clone(const sdrgpu_fir* h, sdrgpu_fir** out);   /* #[derive(Clone)] Fir, fir.rs:6 */
 void sdrgpu_fir_destroy(sdrgpu_fir* h);
@@ -159,6 +163,7 @@ int sdrgpu_firbank_process(sdrgpu_firbank* h, const void* in, size_t ld_in, size
 int sdrgpu_firbank_process_dev(sdrgpu_firbank* h, const void* d_in, size_t ld_in,
                                size_t n_in, void* d_out, size_t ld_out, size_t* n_out);
 int sdrgpu_firbank_sync(sdrgpu_firbank* h);
+int sdrgpu_firbank_last_algorithm(const sdrgpu_firbank* h, int* algo);
 int sdrgpu_firbank_reset(sdrgpu_firbank* h);
 int sdrgpu_firbank_clone(const sdrgpu_firbank* h, sdrgpu_firbank** out);
 void sdrgpu_firbank_destroy(sdrgpu_firbank* h);

@@ -299,3 +299,27 @@ def test_time_shard_halo_equivalence(sdr, oracle, algo):
     if algo == "direct":
         assert np.array_equal(y2, whole[half // 4:])
     assert_parity(y2, oracle.Fir(taps, 4, sample_kind=1).process(x)[half // 4:])
+
+
+@pytest.mark.parametrize("weak", [1e-3, 1e-6])
+def test_fir_mx_intra_window_dynamic_range(sdr, oracle, weak):
+    """A strong burst next to a weak tone inside one staging window of the fp16-split
+    kernel (its per-tile scale follows the burst): every 64-output window -- including the
+    weak-only ones whose tile shares the burst's scale -- is judged against its OWN RMS."""
+    from sdrgpu import _lib
+    import scipy.signal as ss
+    n, D = 1 << 16, 4
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    t = np.arange(n)
+    x = (weak * np.exp(2j * np.pi * 0.01 * t)).astype(np.complex64)
+    for b0 in range(3000, n, 9000):           # 1.0 bursts, 64 samples long
+        x[b0:b0 + 64] += np.exp(2j * np.pi * 0.013 * t[b0:b0 + 64]).astype(np.complex64)
+    ref = oracle.Fir(taps, D, sample_kind=1).process(x)
+    f = fir(sdr, taps, 1, D, "mx")
+    y = f.process(x)
+    assert f.last_algorithm() == _lib.FIR_MATRIX
+    worst = 0.0
+    for w0 in range(0, ref.size - 64, 64):
+        mx, _ = rms_rel_err(y[w0:w0 + 64], ref[w0:w0 + 64])
+        worst = max(worst, mx)
+    assert worst <= 1e-5, f"worst 64-output window max/rms {worst:.3e} (weak {weak})"

@@ -31,6 +31,7 @@ struct FirCore {
     int K = 1, D = 1;
     size_t nch = 1;
     int algo = SDRGPU_FIR_AUTO;
+    int last_algo = SDRGPU_FIR_AUTO;       // path that ran the most recent block
     std::vector<unsigned char> taps_host;  // original taps (for clone / OS prep)
     int tpp = 0;
     void* d_taps_pm = nullptr;
@@ -187,6 +188,7 @@ struct FirCore {
         p.nch = (int)nch;
         p.force_naive = 0;
         int st = SDRGPU_ERR_UNSUPPORTED;
+        int ran = SDRGPU_FIR_MATRIX;
         if (want_mx()) {
             if (!mx_state && mx_status == SDRGPU_OK)
                 mx_state = fir_mx_prepare(device, reinterpret_cast<const float*>(taps_host.data()),
@@ -213,14 +215,19 @@ struct FirCore {
             }
         }
         if (st != SDRGPU_OK && want_os()) {
+            ran = SDRGPU_FIR_OVERLAP_SAVE;
             if (!os_state && os_status == SDRGPU_OK)
                 os_state = fir_os_prepare(device, csk, tk, taps_host.data(), K, D, stream.cur,
                                           &os_status);
             if (os_state) st = fir_os_launch(p, os_state, stream.cur);
             if (st != SDRGPU_OK && algo == SDRGPU_FIR_OVERLAP_SAVE) return st;
         }
-        if (st != SDRGPU_OK) st = fir_direct_launch(p, stream.cur);
+        if (st != SDRGPU_OK) {
+            ran = SDRGPU_FIR_DIRECT;
+            st = fir_direct_launch(p, stream.cur);
+        }
         if (st) return st;
+        last_algo = ran;
         if (K > 1) cur ^= 1;
         seen += n_in;
         return SDRGPU_OK;
@@ -399,6 +406,12 @@ int sdrgpu_fir_sync(sdrgpu_fir* h) {
     return h->core.sync_all();
 }
 
+int sdrgpu_fir_last_algorithm(const sdrgpu_fir* h, int* algo) {
+    if (!h || !algo) return SDRGPU_ERR_INVALID;
+    *algo = h->core.last_algo;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_fir_reset(sdrgpu_fir* h) {
     if (!h) return SDRGPU_ERR_INVALID;
     return h->core.reset_state();
@@ -495,6 +508,12 @@ int sdrgpu_firbank_sync(sdrgpu_firbank* h) {
     if (!h) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->core.device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->core.stream.cur));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_last_algorithm(const sdrgpu_firbank* h, int* algo) {
+    if (!h || !algo) return SDRGPU_ERR_INVALID;
+    *algo = h->core.last_algo;
     return SDRGPU_OK;
 }
 

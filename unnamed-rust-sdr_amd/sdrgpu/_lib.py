@@ -96,6 +96,7 @@ SIGNATURES = [
     ("sdrgpu_fir_process_dev", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_process_async", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_sync", c_int, [_H]),
+    ("sdrgpu_fir_last_algorithm", c_int, [_H, POINTER(c_int)]),
     ("sdrgpu_fir_reset", c_int, [_H]),
     ("sdrgpu_fir_clone", c_int, [_H, _PH]),
     ("sdrgpu_fir_destroy", None, [_H]),
@@ -111,6 +112,7 @@ SIGNATURES = [
     ("sdrgpu_firbank_process_dev", c_int,
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_firbank_sync", c_int, [_H]),
+    ("sdrgpu_firbank_last_algorithm", c_int, [_H, POINTER(c_int)]),
     ("sdrgpu_firbank_reset", c_int, [_H]),
     ("sdrgpu_firbank_clone", c_int, [_H, _PH]),
     ("sdrgpu_firbank_destroy", None, [_H]),

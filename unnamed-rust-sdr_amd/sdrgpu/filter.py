@@ -183,6 +183,12 @@ class FirFilter:
     def sync(self):
         check(lib().sdrgpu_fir_sync(self._h), "sdrgpu_fir_sync")
 
+    def last_algorithm(self) -> int:
+        """FIR_DIRECT / FIR_OVERLAP_SAVE / FIR_MATRIX: the path of the last block."""
+        a = ctypes.c_int()
+        check(lib().sdrgpu_fir_last_algorithm(self._h, ctypes.byref(a)), "last_algorithm")
+        return a.value
+
 
 class FirBank:
     """nch independent Fir<C,A> (fir.rs:6-32) sharing taps; channel-major blocks."""
@@ -269,6 +275,11 @@ class FirBank:
 
     def sync(self):
         check(lib().sdrgpu_firbank_sync(self._h), "sdrgpu_firbank_sync")
+
+    def last_algorithm(self) -> int:
+        a = ctypes.c_int()
+        check(lib().sdrgpu_firbank_last_algorithm(self._h, ctypes.byref(a)), "last_algorithm")
+        return a.value
 
 
 # --------------------------------------------------------------------------- Biquad
