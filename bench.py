@@ -6,10 +6,12 @@ f32 IQ (nominal 2.4 Msps stream -> 600 ksps), single channel per GPU, 2^28 input
 per step, inputs resident in HBM.  One step = one sdrgpu_fir_process_dev() call over the
 whole batch (the FIR state carries across steps, as a stream would).
 
-Multi-GPU (torchrun, one process per GPU): each rank filters its own time shard of the
-stream (weak scaling; no data-path collective -- SURVEY.md 8e).  Timing: barrier +
-synchronize on both sides of exactly K steps, MAX over ranks; value = all ranks' samples
-/ that time.
+Multi-GPU (one process per GPU): each rank filters its own time shard of the stream (weak
+scaling; no data-path collective -- SURVEY.md 8e).  Under torch.distributed.run the ranks
+come from the environment (WORLD_SIZE must equal --gpus); a plain `python bench.py --gpus
+N` spawns the N rank processes itself (before anything touches the GPU) and relays rank
+0's line.  Timing: barrier + synchronize on both sides of exactly K steps, MAX over ranks;
+value = all ranks' samples / that time.
 
 Also reported (rank 0, N=1 only unless --cpu-baseline force):
   roofline      algorithmic bytes per launch (10 B / input sample) / the
@@ -22,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -60,6 +64,50 @@ def synth_iq_pattern(n, seed):
     return x.astype(np.complex64)
 
 
+def host_info():
+    """Host CPU the baseline ran on (nproc and the /proc/cpuinfo model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, timeout=None):
+    """Run `script argv` as n rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    set, rendezvous on 127.0.0.1), relay their output, return the worst exit status.  The
+    parent never touches the GPU: every rank is a fresh process."""
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate(timeout=timeout)[0]
+    rcs = [procs[0].returncode] + [p.wait(timeout=timeout) for p in procs[1:]]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def cpu_baseline(taps, seconds):
     """Oracle (restated reference path: all outputs computed, 3 of 4 dropped) on 1 core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -77,7 +125,7 @@ def cpu_baseline(taps, seconds):
         if el >= seconds:
             break
     return {"value": done / el / 1e6, "unit": "complex Msamples/s", "cores": 1,
-            "kind": "port",
+            "kind": "port", "host": host_info(),
             "sample": f"{done} c64 samples ({done // chunk} blocks of 2^18) through the oracle "
                       f"Fir(255 taps)+Decimate(4), {el:.1f} s on 1 host core"}
 
@@ -114,7 +162,11 @@ def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

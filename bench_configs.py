@@ -204,6 +204,18 @@ def bench_c2pinned(args):
     return res
 
 
+def spot_check(pyoracle, taps, x, y, ch, n, m=4096):
+    """Channel `ch` of a D = 1 bank whose every step filtered the same resident block:
+    the state entering a step is the block's own last K-1 samples (the steady state)."""
+    K = len(taps)
+    tail = x.download(K - 1, offset_bytes=8 * (ch * n + n - (K - 1)))
+    xin = x.download(m, offset_bytes=8 * ch * n)
+    ref = pyoracle.Fir(taps, 1, sample_kind=1).process(np.concatenate([tail, xin]))[K - 1:]
+    got = y.download(m, offset_bytes=8 * ch * n)
+    return float(np.abs(got.astype(np.complex128) - ref).max() /
+                 np.sqrt(np.mean(np.abs(ref.astype(np.complex128)) ** 2)))
+
+
 # ------------------------------------------------------------------------------ c4
 def bench_c4(args):
     import scipy.signal as ss
@@ -231,16 +243,18 @@ def bench_c4(args):
     # split: matched filter alone
     _, ms_fir = time_events(lambda: bank.process_dev(x.ptr, n, n, mf.ptr, n), bank.stream(),
                             args.steps, 0, lambda: (bank.sync(), synchronize()))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
     units = nch * n
+    fir_check = spot_check(pyoracle, taps, x, mf, nch // 3, n)
+    assert fir_check <= 1e-5, fir_check
     res = {"config": f"c4: 255-tap matched filter + PLL FM demod (src/main.rs:41-46), {nch} ch x 2^{args.c4_log2n}",
            "metric": "complex Msamples/s (input, all channels)", "value": round(units / (ms * 1e-3) / 1e6, 1),
            "roofline": roof(12, units, ms), "fir_ms": round(ms_fir, 3), "pll_ms": round(ms - ms_fir, 3),
            "pll_ns_per_sample_chain": round((ms - ms_fir) * 1e6 / n, 2),
            "note": "PLL is bound by its loop-carried latency (ns per sample per channel chain), not HBM",
-           "wall_ms_per_step": round(wall * 1e3, 3)}
+           "wall_ms_per_step": round(wall * 1e3, 3), "fir_spot_check_max_over_rms": fir_check}
     if not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle
         cores = min(os.cpu_count() or 1, 16)
         cn, cl = cores, 1 << 14
         xs = cplx_pattern(cn * cl, 8).reshape(cn, cl)
@@ -251,8 +265,9 @@ def bench_c4(args):
             pyoracle.pll_batch(p, m, nthreads=cores)
             done += cn * cl
         el = time.perf_counter() - t0
+        from bench import host_info
         res["cpu_baseline"] = {"value": round(done / el / 1e6, 2), "unit": "complex Msamples/s",
-                               "cores": cores, "kind": "port",
+                               "cores": cores, "kind": "port", "host": host_info(),
                                "sample": f"{done} samples ({cn} ch x 2^14 blocks) oracle FIR+PLL, {el:.1f} s"}
     return res
 
@@ -295,27 +310,48 @@ def bench_c5(args):
            "metric": "complex Msamples/s (input, all ranks)",
            "value": round(nch_total * n / (t[0] * 1e-3) / 1e6, 1) if world > 1 else round(nch * n / (ms * 1e-3) / 1e6, 1),
            "roofline_rank0": roof(16, nch * n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
-    if dist is not None and nch_total % world == 0:
-        # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately)
+    # spot-check one resident channel against the oracle (the rate is of checked outputs)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    ck = nch // 2
+    res["spot_check_max_over_rms"] = spot_check(pyoracle, taps, x, y, ck, n)
+    assert res["spot_check_max_over_rms"] <= 1e-5, res["spot_check_max_over_rms"]
+    if dist is not None:
+        # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately);
+        # uneven channel blocks (nch % world != 0) go through grouped send / recv
         ids = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         comm = Comm(local, world, rank, ids[0])
-        blk = nch * n * 8
-        full = DeviceBuffer(blk * world, local) if rank == 0 else None
+        sizes = [(b - a) * n * 8 for a, b in (channel_range(nch_total, world, r) for r in range(world))]
+        full = DeviceBuffer(sum(sizes), local) if rank == 0 else None
         s = bank.stream()
         from sdrgpu.device import Event
         e0, e1, e2 = Event(local), Event(local), Event(local)
         comm.barrier(s)
         e0.record(s)
-        comm.scatter(full.ptr if full else None, x.ptr, blk, 0, s)
+        comm.scatterv(full.ptr if full else None, x.ptr, sizes, 0, s)
         e1.record(s)
-        comm.gather(y.ptr, full.ptr if full else None, blk, 0, s)
+        comm.gatherv(y.ptr, full.ptr if full else None, sizes, 0, s)
         e2.record(s)
         bank.sync()
         res["rccl_scatter_ms"] = round(e0.elapsed_ms(e1), 3)
         res["rccl_gather_ms"] = round(e1.elapsed_ms(e2), 3)
         res["end_to_end_value"] = round(nch_total * n / ((t[0] + e0.elapsed_ms(e2)) * 1e-3) / 1e6, 1)
         comm.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = min(os.cpu_count() or 1, 16)
+        cn, cl = 4 * cores, 1 << 14
+        xs = cplx_pattern(cn * cl, 9).reshape(cn, cl)
+        t0, done = time.perf_counter(), 0
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            pyoracle.fir_batch(taps, xs, 1, nthreads=cores)
+            done += cn * cl
+        el = time.perf_counter() - t0
+        from bench import host_info
+        res["cpu_baseline"] = {"value": round(done / el / 1e6, 2), "unit": "complex Msamples/s",
+                               "cores": cores, "kind": "port", "host": host_info(),
+                               "sample": f"{done} samples ({cn} ch x 2^14 blocks) through the "
+                                         f"oracle Fir (255 taps, one Fir per channel), {el:.1f} s"}
     if dist is not None:
         dist.destroy_process_group()
     return res if rank == 0 else None

@@ -373,6 +373,13 @@ int sdrgpu_comm_scatter(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t
 /* rank i's block lands at d_recv + i*bytes_per_rank on root */
 int sdrgpu_comm_gather(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t bytes_per_rank,
                        int root, void* hip_stream);
+/* Uneven channel blocks (nch % nranks != 0): bytes[r] / displs[r] (nranks host entries,
+ * the same on every rank) give rank r's block size and its offset in the root's buffer.
+ * Grouped point-to-point sends from / receives to the root (ncclSend / ncclRecv). */
+int sdrgpu_comm_scatterv(sdrgpu_comm* c, const void* d_send, const size_t* bytes,
+                         const size_t* displs, void* d_recv, int root, void* hip_stream);
+int sdrgpu_comm_gatherv(sdrgpu_comm* c, const void* d_send, void* d_recv, const size_t* bytes,
+                        const size_t* displs, int root, void* hip_stream);
 int sdrgpu_comm_barrier(sdrgpu_comm* c, void* hip_stream);
 void sdrgpu_comm_destroy(sdrgpu_comm* c);
 

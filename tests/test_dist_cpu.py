@@ -54,3 +54,40 @@ def test_shard_ranges(sdr):
         rs = [time_range(n, world, r, align) for r in range(world)]
         assert rs[0][0] == 0 and rs[-1][1] == n
         assert all(lo % align == 0 for lo, _ in rs)
+
+
+def test_launch_ranks_spawns_world(capsys):
+    """`bench.py --gpus N` without torchrun starts N rank processes itself (the driver's
+    N-GPU invocation shape) and relays rank 0's JSON line."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    probe = os.path.join(ROOT, "tests", "_rank_probe.py")
+    rc = bench.launch_ranks(3, ["--steps", "2"], script=probe, timeout=120)
+    out = capsys.readouterr().out.strip().splitlines()[-1]
+    d = json.loads(out)
+    assert rc == 0 and d["world"] == 3
+    assert sorted(r["rank"] for r in d["ranks"]) == [0, 1, 2]
+    assert [r["local"] for r in sorted(d["ranks"], key=lambda r: r["rank"])] == [0, 1, 2]
+    assert all(r["argv"] == ["--steps", "2"] for r in d["ranks"])
+    assert len({r["el"] for r in d["ranks"]}) == 1   # max-over-ranks time on every rank
+
+
+def test_launch_ranks_propagates_failure(capsys):
+    sys.path.insert(0, ROOT)
+    import bench
+    probe = os.path.join(ROOT, "tests", "_rank_probe.py")
+    os.environ["PROBE_EXIT_RANK"] = "1"
+    try:
+        rc = bench.launch_ranks(2, [], script=probe, timeout=120)
+    finally:
+        del os.environ["PROBE_EXIT_RANK"]
+    assert rc == 3
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

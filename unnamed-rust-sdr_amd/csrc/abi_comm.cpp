@@ -77,6 +77,61 @@ int sdrgpu_comm_gather(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t 
                                   static_cast<hipStream_t>(stream)));
 }
 
+// Uneven blocks (nch % nranks != 0): point-to-point sends from / to the root inside one
+// RCCL group (every link of the root's xGMI fan-out is driven at once); the root's own
+// block is a device-local copy.  bytes / displs: nranks host entries, identical on all ranks.
+int sdrgpu_comm_scatterv(sdrgpu_comm* c, const void* d_send, const size_t* bytes,
+                         const size_t* displs, void* d_recv, int root, void* stream) {
+    if (!c || !bytes || root < 0 || root >= c->nranks) return SDRGPU_ERR_INVALID;
+    if (c->rank == root && (!d_send || !displs)) return SDRGPU_ERR_INVALID;
+    if (bytes[c->rank] && !d_recv) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(c->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const char* src = static_cast<const char*>(d_send);
+    int st = nccl_status(ncclGroupStart());
+    if (st) return st;
+    if (c->rank == root) {
+        for (int r = 0; r < c->nranks; ++r)
+            if (r != root && bytes[r])
+                if ((st = nccl_status(ncclSend(src + displs[r], bytes[r], ncclUint8, r, c->comm, s))))
+                    break;
+    } else if (bytes[c->rank]) {
+        st = nccl_status(ncclRecv(d_recv, bytes[c->rank], ncclUint8, root, c->comm, s));
+    }
+    const int end = nccl_status(ncclGroupEnd());
+    if (st || end) return st ? st : end;
+    if (c->rank == root && bytes[root])
+        SDRGPU_HIP_TRY(hipMemcpyAsync(d_recv, src + displs[root], bytes[root],
+                                      hipMemcpyDeviceToDevice, s));
+    return SDRGPU_OK;
+}
+
+int sdrgpu_comm_gatherv(sdrgpu_comm* c, const void* d_send, void* d_recv, const size_t* bytes,
+                        const size_t* displs, int root, void* stream) {
+    if (!c || !bytes || root < 0 || root >= c->nranks) return SDRGPU_ERR_INVALID;
+    if (c->rank == root && (!d_recv || !displs)) return SDRGPU_ERR_INVALID;
+    if (bytes[c->rank] && !d_send) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(c->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char* dst = static_cast<char*>(d_recv);
+    int st = nccl_status(ncclGroupStart());
+    if (st) return st;
+    if (c->rank == root) {
+        for (int r = 0; r < c->nranks; ++r)
+            if (r != root && bytes[r])
+                if ((st = nccl_status(ncclRecv(dst + displs[r], bytes[r], ncclUint8, r, c->comm, s))))
+                    break;
+    } else if (bytes[c->rank]) {
+        st = nccl_status(ncclSend(d_send, bytes[c->rank], ncclUint8, root, c->comm, s));
+    }
+    const int end = nccl_status(ncclGroupEnd());
+    if (st || end) return st ? st : end;
+    if (c->rank == root && bytes[root])
+        SDRGPU_HIP_TRY(hipMemcpyAsync(dst + displs[root], d_send, bytes[root],
+                                      hipMemcpyDeviceToDevice, s));
+    return SDRGPU_OK;
+}
+
 int sdrgpu_comm_barrier(sdrgpu_comm* c, void* stream) {
     if (!c) return SDRGPU_ERR_INVALID;
     DeviceGuard g(c->device);

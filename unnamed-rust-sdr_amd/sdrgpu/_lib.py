@@ -183,6 +183,8 @@ SIGNATURES = [
     ("sdrgpu_comm_init", c_int, [c_int, c_int, c_int, c_void_p, _PH]),
     ("sdrgpu_comm_scatter", c_int, [_H, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("sdrgpu_comm_gather", c_int, [_H, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    ("sdrgpu_comm_scatterv", c_int, [_H, c_void_p, _PS, _PS, c_void_p, c_int, c_void_p]),
+    ("sdrgpu_comm_gatherv", c_int, [_H, c_void_p, c_void_p, _PS, _PS, c_int, c_void_p]),
     ("sdrgpu_comm_barrier", c_int, [_H, c_void_p]),
     ("sdrgpu_comm_destroy", None, [_H]),
 ]

@@ -53,6 +53,25 @@ class Comm:
         check(lib().sdrgpu_comm_gather(self._h, d_send, d_recv, bytes_per_rank, root, stream),
               "sdrgpu_comm_gather")
 
+    def _counts(self, bytes_per_rank):
+        n = self.nranks
+        assert len(bytes_per_rank) == n
+        b = (ctypes.c_size_t * n)(*bytes_per_rank)
+        d = (ctypes.c_size_t * n)(*[sum(bytes_per_rank[:r]) for r in range(n)])
+        return b, d
+
+    def scatterv(self, d_send: int, d_recv: int, bytes_per_rank, root: int = 0, stream=None):
+        """Uneven blocks: rank r receives bytes_per_rank[r] bytes, packed in rank order in
+        the root's buffer."""
+        b, d = self._counts(bytes_per_rank)
+        check(lib().sdrgpu_comm_scatterv(self._h, d_send, b, d, d_recv, root, stream),
+              "sdrgpu_comm_scatterv")
+
+    def gatherv(self, d_send: int, d_recv: int, bytes_per_rank, root: int = 0, stream=None):
+        b, d = self._counts(bytes_per_rank)
+        check(lib().sdrgpu_comm_gatherv(self._h, d_send, d_recv, b, d, root, stream),
+              "sdrgpu_comm_gatherv")
+
     def barrier(self, stream=None):
         check(lib().sdrgpu_comm_barrier(self._h, stream), "sdrgpu_comm_barrier")
 
