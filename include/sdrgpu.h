@@ -175,8 +175,11 @@ void sdrgpu_firbank_destroy(sdrgpu_firbank* h);
  * exec transforms `count` back-to-back frames of n C64 samples; out[i] of each frame is
  * X[(i - n/2) mod n] / sqrt(n) (fft.rs:14-26).  Frequencies (fft.rs:18,24) are
  * (i - n/2) * rate / n and are produced host-side by sdrgpu_fft_freqs.
- * n must be a power of two, 2 <= n <= 2^20 (rustfft accepts any n: other sizes return
- * SDRGPU_ERR_UNSUPPORTED).
+ * Any n >= 1 plans, as rustfft's FFTplanner does (fft.rs:10-11): powers of two up to 2^20
+ * run the Stockham / four-step kernels; other n whose prime factors are all <= 13 run
+ * mixed-radix tiles (n <= 4096) or a mixed-radix four-step (n = n1*n2, both <= 4096); the
+ * rest run Bluestein over a power-of-two convolution (n <= 2^19).  Larger n:
+ * SDRGPU_ERR_UNSUPPORTED.
  * ===================================================================================== */
 typedef struct sdrgpu_fft sdrgpu_fft;
 
@@ -185,7 +188,8 @@ int sdrgpu_fft_set_stream(sdrgpu_fft* h, void* hip_stream);
 int sdrgpu_fft_get_stream(const sdrgpu_fft* h, void** hip_stream);
 int sdrgpu_fft_exec(sdrgpu_fft* h, const void* in, void* out, size_t count);
 int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t count);
-/* rfft: `count` frames of n F32 samples -> count frames of n/2 C64 bins [n/2, n). */
+/* rfft: `count` frames of n F32 samples -> count frames of n - n/2 C64 values: the collated
+ * output with its first n/2 entries drained (fft.rs:35), i.e. X[0 .. n - n/2) * 1/sqrt(n). */
 int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count);
 int sdrgpu_fft_sync(sdrgpu_fft* h);
 void sdrgpu_fft_destroy(sdrgpu_fft* h);

@@ -390,17 +390,28 @@ static void dft_f64(c64d* a, size_t n) {
             }
         }
     } else {
+        /* direct DFT (any n): W_n^m from a table of the same f64 cos/sin values */
         c64d* t = (c64d*)malloc(sizeof(c64d) * n);
+        double* cs = (double*)malloc(sizeof(double) * 2 * n);
+        for (size_t m = 0; m < n; ++m) {
+            double ang = -2.0 * M_PI * (double)m / (double)n;
+            cs[2 * m] = cos(ang);
+            cs[2 * m + 1] = sin(ang);
+        }
         for (size_t k = 0; k < n; ++k) {
             double sr = 0, si = 0;
+            size_t m = 0;
             for (size_t j = 0; j < n; ++j) {
-                double ang = -2.0 * M_PI * (double)((k * j) % n) / (double)n;
-                sr += a[j].re * cos(ang) - a[j].im * sin(ang);
-                si += a[j].re * sin(ang) + a[j].im * cos(ang);
+                double c = cs[2 * m], sn = cs[2 * m + 1];
+                sr += a[j].re * c - a[j].im * sn;
+                si += a[j].re * sn + a[j].im * c;
+                m += k;
+                if (m >= n) m -= n;
             }
             t[k].re = sr; t[k].im = si;
         }
         memcpy(a, t, sizeof(c64d) * n);
+        free(cs);
         free(t);
     }
 }

@@ -15,6 +15,11 @@ Inputs are seeded; each fixture is a small .npz (no pickles).
   resample.npz    libsamplerate ZOH / linear (src/resample.rs) from the closed form with
                   exact rational positions q_k = k / ratio - 1 (x[-1] = x[0] after reset),
                   not the serial f64 walk the oracle restates
+  fft_any.npz     fft::fft / rfft at lengths that are not powers of two (rustfft plans any
+                  N, src/fft.rs:10-11): the reference's own callers' 1000-point window
+                  (examples/live.rs:30) and 14,400-point rfft (examples/fft.rs:64,78 at
+                  144 kHz), plus 1001 = 7*11*13, primes 17 / 1009 / 4099, 6, 12288; and a
+                  1000-point STFT (Window + Decimate) over a short stream
 """
 from fractions import Fraction
 import os
@@ -108,6 +113,33 @@ def main():
         cases[f"lin{ci}"], cases[f"linamb{ci}"] = src_closed_form(xr, ratio, True)
         cases[f"zoh{ci}"], cases[f"zohamb{ci}"] = src_closed_form(xr, ratio, False)
     np.savez(os.path.join(HERE, "resample.npz"), ncases=5, **cases)
+
+    # any-N fft::fft (numpy fftshift rolls by N // 2 = the reference's -(N/2) start, odd N too)
+    anyn = {}
+    sizes = (6, 17, 1000, 1001, 1009, 4099, 12288, 14400)
+    for N in sizes:
+        xf = cplx(rng, N)
+        anyn[f"x{N}"] = xf
+        anyn[f"y{N}"] = np.fft.fftshift(np.fft.fft(xf.astype(np.complex128))) / np.sqrt(N)
+    # rfft (fft.rs:30-37): collated output with the first N/2 entries drained
+    for N in (1001, 14400):
+        xr = rng.standard_normal(N).astype(np.float32)
+        full = np.fft.fftshift(np.fft.fft(xr.astype(np.complex128))) / np.sqrt(N)
+        anyn[f"rx{N}"] = xr
+        anyn[f"ry{N}"] = full[N // 2:]
+    # 1000-point STFT, hop 300 (live.rs window(1000/rate).decimate(fps))
+    N, hop = 1000, 300
+    xs = cplx(rng, 3000 + 77)
+    nf = xs.size // hop
+    Y = np.zeros((nf, N), np.complex128)
+    for j in range(nf):
+        beg = (j + 1) * hop - N
+        fr = np.zeros(N, np.complex128)
+        lo = max(0, beg)
+        fr[lo - beg:] = xs[lo:beg + N]
+        Y[j] = np.fft.fftshift(np.fft.fft(fr)) / np.sqrt(N)
+    anyn.update(sx=xs, sn=N, shop=hop, sy=Y)
+    np.savez(os.path.join(HERE, "fft_any.npz"), sizes=np.array(sizes), **anyn)
 
 
 def src_closed_form(x, ratio, linear):

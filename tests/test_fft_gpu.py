@@ -50,14 +50,86 @@ def test_rfft(sdr, oracle):
         f, y = sdr.fft.rfft(x, 48000.0)
         ref = oracle.fft_frame(x.astype(np.complex64))[n // 2:]
         assert_parity(y, ref, what=f"rfft {n}")
-        assert f[0] == 0.0 and len(f) == n // 2
+        assert f[0] == 0.0 and len(f) == n - n // 2
 
 
-def test_fft_non_pow2_unsupported(sdr):
-    from sdrgpu import _lib
-    with pytest.raises(_lib.SdrGpuError) as e:
-        sdr.fft.FftPlan(1000)
-    assert e.value.code == _lib.ERR_UNSUPPORTED
+# lengths that are not powers of two: mixed-radix tiles (smooth, <= 4096), mixed-radix
+# four-step (smooth, > 4096) and Bluestein (a prime factor > 13)
+ANY_N = [1, 3, 5, 6, 7, 9, 12, 17, 100, 1000, 1001, 1009, 1331, 2187, 3000, 4095, 4099,
+         6561, 12288, 14400, 15625, 30030, 65537, 100000, 262139]
+
+
+@pytest.mark.parametrize("n", ANY_N)
+def test_fft_any_size(sdr, oracle, n):
+    rng = np.random.default_rng(n + 7)
+    count = max(1, min(5, 20000 // n))
+    x = cplx(rng, n * count).reshape(count, n)
+    y = sdr.fft.FftPlan(n).exec(x)
+    for c in range(count if n <= 20000 else 1):
+        ref = oracle.fft_frame(x[c]) if n <= 20000 else \
+            (np.fft.fftshift(np.fft.fft(x[c].astype(np.complex128))) / np.sqrt(n))
+        assert_parity(y[c], ref, what=f"n={n} frame {c}")
+
+
+def test_fft_any_golden(sdr):
+    """examples/live.rs:30's 1000-point and examples/fft.rs:64,78's 14,400-point transforms
+    (and 1001, primes, 6, 12288) against NumPy float64 fixtures."""
+    g = np.load(os.path.join(GOLD, "fft_any.npz"), allow_pickle=False)
+    for n in g["sizes"]:
+        _, y = sdr.fft.fft(g[f"x{n}"], 1.0)
+        assert_parity(y, g[f"y{n}"], what=f"golden fft {n}")
+    for n in (1001, 14400):
+        f, y = sdr.fft.rfft(g[f"rx{n}"], 144000.0)
+        assert y.shape == (n - n // 2,) and f.shape == y.shape
+        assert_parity(y, g[f"ry{n}"], what=f"golden rfft {n}")
+    y = sdr.fft.Stft(int(g["sn"]), int(g["shop"])).process(g["sx"])
+    assert_parity(y, g["sy"], what="golden stft 1000")
+
+
+@pytest.mark.parametrize("n", [1000, 1001, 14400, 4099, 65536])
+def test_rfft_any_size(sdr, oracle, n):
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal((3, n)).astype(np.float32)
+    y = sdr.fft.FftPlan(n).exec_real(x)
+    assert y.shape == (3, n - n // 2)
+    for c in range(3):
+        ref = np.fft.fftshift(np.fft.fft(x[c].astype(np.complex128)))[n // 2:] / np.sqrt(n)
+        assert_parity(y[c], ref, what=f"rfft n={n} frame {c}")
+
+
+@pytest.mark.parametrize("n,hop", [(1000, 400), (1000, 1000), (1001, 333), (14400, 7200),
+                                   (4099, 2048)])
+def test_stft_any_size_streaming(sdr, oracle, n, hop):
+    rng = np.random.default_rng(n * 3 + hop)
+    total = hop * 7 + 55
+    x = cplx(rng, total)
+    ref = oracle.stft(x, n, hop, nthreads=8)
+    s = sdr.fft.Stft(n, hop)
+    parts, i = [], 0
+    for step in (1, hop - 1, 5, 2 * hop + 3):
+        parts.append(s.process(x[i:i + step]))
+        i += step
+    parts.append(s.process(x[i:]))
+    y = np.concatenate([p for p in parts if p.size], axis=0)
+    assert y.shape == ref.shape
+    for j in range(ref.shape[0]):
+        assert_parity(y[j], ref[j], what=f"n={n} hop={hop} frame {j}")
+
+
+def test_fft_many_frames_batching(sdr, oracle):
+    """Enough frames that the four-step / Bluestein plans run several scratch batches."""
+    from sdrgpu.device import DeviceBuffer
+    for n, count in ((14400, 2400), (4099, 4500)):
+        rng = np.random.default_rng(n)
+        x = cplx(rng, n * count)
+        p = sdr.fft.FftPlan(n)
+        dx = DeviceBuffer.from_numpy(x)
+        dy = DeviceBuffer.empty(n * count)
+        p.exec_dev(dx.ptr, dy.ptr, count)
+        p.sync()
+        for c in (0, count // 2, count - 1):
+            y = dy.download(n, offset_bytes=8 * n * c)
+            assert_parity(y, oracle.fft_frame(x[c * n:(c + 1) * n]), what=f"n={n} frame {c}")
 
 
 def test_stft_golden(sdr):

@@ -80,6 +80,20 @@ def test_oracle_fft_golden(oracle):
         assert_parity(y, g[f"y{N}"], 1e-6, f"fft N={N}")
 
 
+def test_oracle_fft_any_n_golden(oracle):
+    """Lengths that are not powers of two (rustfft plans any N, src/fft.rs:10-11), odd N's
+    collation start -(N/2) included, rfft's drain (fft.rs:35) and a 1000-point STFT."""
+    g = load("fft_any.npz")
+    for N in g["sizes"]:
+        assert_parity(oracle.fft_frame(g[f"x{N}"]), g[f"y{N}"], 1e-6, f"fft N={N}")
+    for N in (1001, 14400):
+        y = oracle.fft_frame(g[f"rx{N}"].astype(np.complex64))[N // 2:]
+        assert_parity(y, g[f"ry{N}"], 1e-6, f"rfft N={N}")
+    y = oracle.stft(g["sx"], int(g["sn"]), int(g["shop"]))
+    assert y.shape == g["sy"].shape
+    assert_parity(y, g["sy"], 1e-6, "stft N=1000")
+
+
 def test_oracle_fft_tone_kat(oracle):
     # fft(freq(rate, f)) has one bin of magnitude sqrt(N) at f (fft.rs:16 norm)
     N, rate = 1024, 1024.0

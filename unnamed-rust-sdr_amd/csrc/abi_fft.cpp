@@ -17,9 +17,9 @@ struct sdrgpu_fft {
     DevBuf stage_in, stage_out, scratch;
 
     int ensure_scratch() {
-        const size_t sf = fft_scratch_frames(plan);
-        if (!sf) return SDRGPU_OK;
-        return scratch.ensure(sf * (size_t)n * sizeof(float2));
+        const size_t b = fft_scratch_bytes(plan);
+        if (!b) return SDRGPU_OK;
+        return scratch.ensure(b);
     }
     void free_all() {
         DeviceGuard g(device);
@@ -70,7 +70,8 @@ extern "C" {
 int sdrgpu_fft_plan(int device, size_t n, sdrgpu_fft** out) {
     if (!out) return SDRGPU_ERR_INVALID;
     *out = nullptr;
-    if (n < 2 || (n & (n - 1)) || n > (1u << 20)) return n == 0 ? SDRGPU_ERR_INVALID : SDRGPU_ERR_UNSUPPORTED;
+    if (n == 0) return SDRGPU_ERR_INVALID;
+    if (n > (1u << 24)) return SDRGPU_ERR_UNSUPPORTED;
     auto* h = new (std::nothrow) sdrgpu_fft();
     if (!h) return SDRGPU_ERR_NOMEM;
     int st = fft_init(h, device, n);
@@ -128,11 +129,10 @@ int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count) {
     if (!h) return SDRGPU_ERR_INVALID;
     if (count == 0) return SDRGPU_OK;
     if (!in || !out) return SDRGPU_ERR_INVALID;
-    if (h->n > 4096) return SDRGPU_ERR_UNSUPPORTED;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
     const size_t in_bytes = count * (size_t)h->n * sizeof(float);
-    const size_t out_bytes = count * (size_t)(h->n / 2) * sizeof(float2);
+    const size_t out_bytes = count * (size_t)(h->n - h->n / 2) * sizeof(float2);
     int st;
     if ((st = h->stage_in.ensure(in_bytes)) || (st = h->stage_out.ensure(out_bytes))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(h->stage_in.ptr, in, in_bytes, hipMemcpyHostToDevice, h->stream.cur));
@@ -172,8 +172,8 @@ int sdrgpu_fft_freqs(size_t n, float rate, float* freqs) {
 int sdrgpu_stft_create(int device, size_t n, size_t hop, sdrgpu_stft** out) {
     if (!out) return SDRGPU_ERR_INVALID;
     *out = nullptr;
-    if (n < 2 || hop == 0) return SDRGPU_ERR_INVALID;
-    if ((n & (n - 1)) || n > (1u << 20)) return SDRGPU_ERR_UNSUPPORTED;
+    if (n == 0 || hop == 0) return SDRGPU_ERR_INVALID;
+    if (n > (1u << 24)) return SDRGPU_ERR_UNSUPPORTED;
     auto* h = new (std::nothrow) sdrgpu_stft();
     if (!h) return SDRGPU_ERR_NOMEM;
     int st = fft_init(&h->fft, device, n);

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "fft_device.hpp"
+#include "fft_frames.hpp"
 #include "fft_kernels.hpp"
 
 namespace sdrgpu {
@@ -35,30 +36,9 @@ constexpr int kTile = 4096;
 __device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
 constexpr int kTileLds = kTile + kTile / 16;
 
-// -------- frame sources ---------------------------------------------------------------
-struct FrameSrc {
-    // mode 0: contiguous frames (frame f at in + f*M)
-    // mode 1: STFT frames from a stream: frame f covers stream [f0 + (f+1)hop - M, +M), stream
-    //         index g < 0 -> hist[g + H] (H = history length) if g >= -H, else 0; g >= n_in -> 0
-    // mode 2: contiguous REAL frames (float, imag = 0) -- rfft
-    int mode;
-    const float2* in;
-    const float* in_real;
-    long n_in;
-    const float2* hist;
-    long H;
-    long first_end;  // stream index (exclusive end) of frame 0 of this launch
-    long hop;
-};
+}  // namespace
 
-__device__ __forceinline__ float2 frame_sample(const FrameSrc& s, long M, long f, long n) {
-    if (s.mode == 0) return s.in[f * M + n];
-    if (s.mode == 2) return make_float2(s.in_real[f * M + n], 0.f);
-    const long g = s.first_end + f * s.hop - M + n;
-    if (g >= 0) return g < s.n_in ? s.in[g] : make_float2(0.f, 0.f);
-    if (g >= -s.H) return s.hist[g + s.H];
-    return make_float2(0.f, 0.f);
-}
+namespace {
 
 // -------- in-place Stockham pass over the 4096-point tile (all sizes compile-time) -----
 // batch of 4096/M transforms of size M; radix R; stride NS.  Each lane does 16/R butterflies.
@@ -138,9 +118,9 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
     }
     __syncthreads();
     tile_fft<M, false>(lds, a.tw);
-    // collated store: out[f][i] = X[(i + M/2) % M] * norm
-    const int half = M / 2;
     if (a.store_mode == 0) {
+        // collated store, output-ordered (coalesced): out[f][i] = X[(i + M/2) % M] * norm
+        const int half = M / 2;
 #pragma unroll 4
         for (int i = 0; i < 16; ++i) {
             const int p = t + kFftBlock * i;
@@ -153,15 +133,11 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
             }
         }
     } else {
-        // rfft: keep collated [M/2, M) = X[0, M/2)
 #pragma unroll 4
         for (int i = 0; i < 16; ++i) {
             const int p = t + kFftBlock * i;
             const int f = p / M, k = p % M;
-            if (f < nf && k < half) {
-                float2 x = lds[fpad(f * M + k)];
-                a.out[(f0 + f) * half + k] = make_float2(x.x * a.norm, x.y * a.norm);
-            }
+            if (f < nf) store_bin(a.out, f0 + f, M, k, lds[fpad(f * M + k)], a.store_mode, a.norm);
         }
     }
 }
@@ -174,6 +150,7 @@ struct FourArgs {
     const float2* tw;       // W_4096
     const float2* twM;      // W_M, M entries
     float norm;
+    int store_mode;
     float2* scratch;        // nframes x M: S[f][n1 * M2 + k2]
     float2* out;
 };
@@ -230,18 +207,13 @@ __global__ __launch_bounds__(kFftBlock) void fft4_pass_b(FourArgs a) {
     }
     __syncthreads();
     tile_fft<M1, false>(lds, a.tw);
-    // X[k2 + M2 k1] -> collated out[(k + M/2) mod M] * norm ; lanes walk k2 (contiguous)
-    float2* O = a.out + f * (long)a.M;
-    const long half = a.M / 2;
+    // X[k2 + M2 k1] by store mode; lanes walk k2 (contiguous)
 #pragma unroll 4
     for (int i = 0; i < 16; ++i) {
         const int p = t + kFftBlock * i;
         const int k1 = p / C, col = p % C;
         const long k = (long)(c0 + col) + (long)a.M2 * k1;
-        long o = k + half;
-        if (o >= a.M) o -= a.M;
-        const float2 x = lds[fpad(col * M1 + k1)];
-        O[o] = make_float2(x.x * a.norm, x.y * a.norm);
+        store_bin(a.out, f, a.M, k, lds[fpad(col * M1 + k1)], a.store_mode, a.norm);
     }
 }
 
@@ -262,6 +234,7 @@ struct F64Args {
     const float2* tw;   // W_4096
     const float2* twM;  // W_65536
     float norm;
+    int store_mode;
     float2* scratch;
     float2* out;
 };
@@ -360,6 +333,12 @@ __global__ __launch_bounds__(16 * CB) void fft64k_pass_b(F64Args a) {
     for (int jj = 0; jj < 16; ++jj) v[jj] = lds[(ka * 16 + jj) * P + r];
     Dft<16, false>::run(v);
     // X[k1 + 256 k2] with k1 = k1b + r, k2 = ka + 16 kb -> collated out[(k + M/2) mod M]
+    if (a.store_mode != 0) {
+#pragma unroll
+        for (int kb = 0; kb < 16; ++kb)
+            store_bin(a.out, f, M, (long)(k1b + r) + 256L * (ka + 16 * kb), v[kb], a.store_mode, a.norm);
+        return;
+    }
     float2* O = a.out + f * M;
     const float nrm = a.norm;
 #pragma unroll
@@ -385,10 +364,23 @@ struct FftPlanDev {
     // next batch's pass A instead of draining the GPU at every pass boundary
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    void* gen = nullptr;  // sizes that are not powers of two (fft_gen.hip)
 };
 
 void* fft_plan_create(int M, int* status) {
-    if (M < 2 || (M & (M - 1)) || M > (1 << 20)) {
+    if (M < 1 || M > (1 << 24)) {
+        *status = SDRGPU_ERR_UNSUPPORTED;
+        return nullptr;
+    }
+    if (M == 1 || (M & (M - 1))) {
+        void* g = fftgen_plan_create(M, status);
+        if (!g) return nullptr;
+        auto* p = new FftPlanDev();
+        p->M = M;
+        p->gen = g;
+        return p;
+    }
+    if (M > (1 << 20)) {
         *status = SDRGPU_ERR_UNSUPPORTED;
         return nullptr;
     }
@@ -428,6 +420,7 @@ void* fft_plan_create(int M, int* status) {
 void fft_plan_destroy(void* plan) {
     auto* p = static_cast<FftPlanDev*>(plan);
     if (!p) return;
+    if (p->gen) fftgen_plan_destroy(p->gen);
     if (p->tw4096) (void)hipFree(p->tw4096);
     if (p->twM) (void)hipFree(p->twM);
     if (p->aux) (void)hipStreamSynchronize(p->aux);
@@ -439,22 +432,32 @@ void fft_plan_destroy(void* plan) {
 
 int fft_plan_size(void* plan) { return static_cast<FftPlanDev*>(plan)->M; }
 
+static size_t frame_scratch_bytes(const FftPlanDev* p) {
+    if (p->gen) return fftgen_frame_scratch_bytes(p->gen);
+    return p->M <= kTile ? 0 : (size_t)p->M * sizeof(float2);
+}
+
+size_t fft_scratch_bytes(void* plan) {
+    return fft_scratch_frames(plan) * frame_scratch_bytes(static_cast<FftPlanDev*>(plan));
+}
+
 size_t fft_scratch_frames(void* plan) {
     auto* p = static_cast<FftPlanDev*>(plan);
-    if (p->M <= kTile) return 0;
+    const size_t per = frame_scratch_bytes(p);
+    if (per == 0) return 0;
     // scratch slab of ~256 MiB (the MALL size): 512 workgroups per pass, 32 launches per 2^28
     // samples; measured 2.79 ms vs 2.92 (128 MiB), 3.08 (64 MiB), 3.23 (512 MiB)
     static const size_t mib = [] {
         const char* e = getenv("SDRGPU_FFT_SLAB_MIB");
         return (size_t)(e ? atoi(e) : 256);
     }();
-    const size_t per = (size_t)p->M * sizeof(float2);
     return std::max<size_t>(1, (mib << 20) / per);
 }
 
 int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
                size_t scratch_frames, hipStream_t s) {
     auto* p = static_cast<FftPlanDev*>(plan);
+    if (p->gen) return fftgen_launch(p->gen, fr, out, store_mode, scratch, scratch_frames, s);
     FrameSrc src;
     src.mode = fr.mode;
     src.in = fr.in;
@@ -494,7 +497,8 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
     }
-    if (store_mode != 0 || !scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
+    if (!scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
+    const long ostride = store_mode == 1 ? p->M - p->M / 2 : p->M;  // output samples per frame
     static const bool use64 = [] {
         const char* e = getenv("SDRGPU_FFT64K");
         return !e || atoi(e) != 0;
@@ -529,6 +533,7 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         a.tw = p->tw4096;
         a.twM = p->twM;
         a.norm = p->norm;
+        a.store_mode = store_mode;
         long bi = 0;
         for (long f0 = 0; f0 < fr.nframes; f0 += batch, ++bi) {
             const long nf = std::min(batch, fr.nframes - f0);
@@ -539,7 +544,7 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
             if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
             else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
             a.nframes = nf;
-            a.out = out + f0 * (long)p->M;
+            a.out = out + f0 * ostride;
             const dim3 g((unsigned)(nf * (256 / cb))), b(16 * cb);
             if (cb == 64 && nt) {
                 hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, st, a);
@@ -574,6 +579,7 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
     a.tw = p->tw4096;
     a.twM = p->twM;
     a.norm = p->norm;
+    a.store_mode = store_mode;
     a.scratch = scratch;
     for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
         const long nf = std::min((long)scratch_frames, fr.nframes - f0);
@@ -581,7 +587,7 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
         else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
         a.nframes = nf;
-        a.out = out + f0 * (long)p->M;
+        a.out = out + f0 * ostride;
         const long ga = nf * (a.M1 / (kTile / a.M2));
         const long gb = nf * (a.M2 / (kTile / a.M1));
         const dim3 bA((unsigned)ga), bB((unsigned)gb), b(kFftBlock);

@@ -1,0 +1,601 @@
+// fft_gen.hip -- fft::fft / fft::rfft / STFT for sizes that are not powers of two (gfx950).
+//
+// rustfft plans any length (reference src/fft.rs:10-11; FFTplanner::new(false) = forward),
+// and the reference's own callers use such lengths: examples/live.rs:30 frames a 1000-point
+// window (window(1000 / rate)) and examples/fft.rs:64,78 rffts take(0.1) of a 144 kHz
+// stream = 14,400 points.  Output semantics are those of fft.hip (collated, x 1/sqrt(N) in
+// f32, fft.rs:14-26; rfft keeps collated [N/2, N), fft.rs:35).
+//
+// Three plans, chosen on the host from N's factorisation:
+//   * mixed-radix tile (N <= 4096, every prime factor <= 13): B = 4096/N transforms per
+//     256-lane workgroup in a ping-pong pair of LDS buffers (64 KiB), one Stockham autosort
+//     pass per radix (16/8/4/2, 3, 5, and a generic odd-radix pair kernel for 7/11/13);
+//     twiddles are loads from a W_N table computed in f64 on the host (no recurrence error);
+//     the STFT frame gather and the collated store are folded into the first / last pass.
+//   * mixed-radix four-step (N > 4096 smooth, N = N1 * N2 with both <= 4096):
+//     pass A = N2-point FFTs down the columns n1 of x[n1 + N1 n2] (rows of C contiguous
+//     samples), x W_N^{n1 k2}, to a scratch slab; pass B = N1-point FFTs over n1 for C'
+//     consecutive k2, stored collated.  Both passes reuse the tile engine.
+//   * Bluestein (a prime factor > 13): X[k] = w[k] sum_n (x[n] w[n]) conj(w[k - n]) with the
+//     chirp w[n] = e^{-i pi n^2 / N} (n^2 mod 2N exact in integers, angle in f64); the
+//     convolution runs as two power-of-two forward FFTs of size M >= 2N - 1 through the
+//     fft.hip kernels (natural-order store) with the chirp spectrum conj(FFT_M(b)) / M
+//     precomputed on the host in f64 (the second transform applies the inverse by
+//     conjugation: IFFT(C) = conj(FFT(conj C)) / M).
+// These are HBM-light, arithmetic-light transforms (no BASELINE config uses them); the
+// power-of-two sizes (configs[2]'s 64 Ki STFT) never come here.
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <vector>
+
+#include "fft_device.hpp"
+#include "fft_frames.hpp"
+#include "fft_kernels.hpp"
+
+namespace sdrgpu {
+
+using namespace fftd;
+
+namespace {
+
+constexpr int kGenBlock = 256;
+constexpr int kGenTile = 4096;   // complex points per LDS buffer
+constexpr int kMaxPass = 16;
+
+struct RadixList {
+    int n = 0;
+    int R[kMaxPass] = {};
+};
+
+// ---- butterflies -----------------------------------------------------------------------
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cfma(float s, float2 a, float2 acc) {
+    return make_float2(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y));
+}
+// a - i b and a + i b
+__device__ __forceinline__ float2 sub_i(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
+__device__ __forceinline__ float2 add_i(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
+
+__device__ __forceinline__ void dft3(float2* v) {
+    constexpr float s = 0.86602540378443865f;  // sin(2 pi / 3)
+    const float2 t1 = cadd(v[1], v[2]);
+    const float2 t2 = make_float2(v[0].x - 0.5f * t1.x, v[0].y - 0.5f * t1.y);
+    const float2 t3 = cscale(csub(v[1], v[2]), s);
+    v[0] = cadd(v[0], t1);
+    v[1] = sub_i(t2, t3);
+    v[2] = add_i(t2, t3);
+}
+
+__device__ __forceinline__ void dft5(float2* v) {
+    constexpr float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;
+    constexpr float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;
+    const float2 a1 = cadd(v[1], v[4]), a2 = cadd(v[2], v[3]);
+    const float2 b1 = csub(v[1], v[4]), b2 = csub(v[2], v[3]);
+    const float2 x0 = v[0];
+    const float2 t1 = cfma(c2, a2, cfma(c1, a1, x0));
+    const float2 t2 = cfma(c1, a2, cfma(c2, a1, x0));
+    const float2 u1 = cfma(s2, b2, cscale(b1, s1));
+    const float2 u2 = cfma(-s1, b2, cscale(b1, s2));
+    v[0] = cadd(x0, cadd(a1, a2));
+    v[1] = sub_i(t1, u1);
+    v[4] = add_i(t1, u1);
+    v[2] = sub_i(t2, u2);
+    v[3] = add_i(t2, u2);
+}
+
+// any odd R: pairs a_m = x_m + x_{R-m}, b_m = x_m - x_{R-m};
+// X_k = x0 + sum_m cos(2 pi mk/R) a_m - i sum_m sin(2 pi mk/R) b_m, X_{R-k} with + i.
+// cos / sin come from the f64-accurate W_N table (R | N): W_N^{j N/R} = cos - i sin.
+template <int R>
+__device__ __forceinline__ void dft_odd(float2* v, const float2* __restrict__ tw, int N) {
+    constexpr int H = (R - 1) / 2;
+    const int st = N / R;
+    float cs[R], sn[R];
+#pragma unroll
+    for (int j = 1; j < R; ++j) {
+        const float2 w = tw[j * st];
+        cs[j] = w.x;
+        sn[j] = -w.y;
+    }
+    float2 a[H + 1], b[H + 1];
+    float2 sum = v[0];
+#pragma unroll
+    for (int m = 1; m <= H; ++m) {
+        a[m] = cadd(v[m], v[R - m]);
+        b[m] = csub(v[m], v[R - m]);
+        sum = cadd(sum, a[m]);
+    }
+    const float2 x0 = v[0];
+#pragma unroll
+    for (int k = 1; k <= H; ++k) {
+        float2 t = x0, u = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 1; m <= H; ++m) {
+            const int j = (m * k) % R;
+            t = cfma(cs[j], a[m], t);
+            u = cfma(sn[j], b[m], u);
+        }
+        v[k] = sub_i(t, u);
+        v[R - k] = add_i(t, u);
+    }
+    v[0] = sum;
+}
+
+template <int R>
+__device__ __forceinline__ void dft_any(float2* v, const float2* __restrict__ tw, int N) {
+    if constexpr (R == 2 || R == 4 || R == 8 || R == 16) Dft<R, false>::run(v);
+    else if constexpr (R == 3) dft3(v);
+    else if constexpr (R == 5) dft5(v);
+    else dft_odd<R>(v, tw, N);
+}
+
+// One Stockham autosort pass over B transforms of size N (transform f at f * N): butterfly
+// (f, j), j < N/R, k = j mod Ns, reads src[f N + j + r N/R], twiddles by W_N^{r k N/(Ns R)}
+// (r k N/(Ns R) < N: a plain table index), writes dst[f N + (j - k) R + k + r Ns].
+template <int R>
+__device__ __forceinline__ void gen_pass(const float2* __restrict__ src, float2* __restrict__ dst,
+                                         int N, int B, int Ns, const float2* __restrict__ tw) {
+    const int Q = N / R;
+    const int total = B * Q;
+    const int step = N / (Ns * R);
+    for (int g = threadIdx.x; g < total; g += kGenBlock) {
+        const int f = g / Q, j = g - f * Q;
+        const int k = j % Ns;
+        const float2* s = src + f * N + j;
+        float2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = s[r * Q];
+        if (Ns > 1) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
+        }
+        dft_any<R>(v, tw, N);
+        float2* d = dst + f * N + (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) d[r * Ns] = v[r];
+    }
+}
+
+// Runs the plan's passes over B transforms of size N held in b0; returns the buffer that
+// holds the natural-order result (b0 or b1).
+__device__ float2* gen_engine(float2* b0, float2* b1, int N, int B, const RadixList& rl,
+                              const float2* __restrict__ tw) {
+    float2* cur = b0;
+    float2* nxt = b1;
+    int Ns = 1;
+    for (int ps = 0; ps < rl.n; ++ps) {
+        const int R = rl.R[ps];
+        switch (R) {
+        case 2: gen_pass<2>(cur, nxt, N, B, Ns, tw); break;
+        case 3: gen_pass<3>(cur, nxt, N, B, Ns, tw); break;
+        case 4: gen_pass<4>(cur, nxt, N, B, Ns, tw); break;
+        case 5: gen_pass<5>(cur, nxt, N, B, Ns, tw); break;
+        case 7: gen_pass<7>(cur, nxt, N, B, Ns, tw); break;
+        case 8: gen_pass<8>(cur, nxt, N, B, Ns, tw); break;
+        case 11: gen_pass<11>(cur, nxt, N, B, Ns, tw); break;
+        case 13: gen_pass<13>(cur, nxt, N, B, Ns, tw); break;
+        default: gen_pass<16>(cur, nxt, N, B, Ns, tw); break;
+        }
+        __syncthreads();
+        float2* t = cur;
+        cur = nxt;
+        nxt = t;
+        Ns *= R;
+    }
+    return cur;
+}
+
+struct GenTileArgs {
+    FrameSrc src;
+    long nframes;
+    int N, B;
+    RadixList rl;
+    const float2* tw;  // W_N, N entries
+    float norm;
+    int store_mode;
+    float2* out;
+};
+
+__global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
+    extern __shared__ float2 glds[];
+    const int N = a.N, B = a.B, L = B * N;
+    float2* b0 = glds;
+    float2* b1 = glds + L;
+    const long f0 = (long)blockIdx.x * B;
+    const int nf = (int)min((long)B, a.nframes - f0);
+    for (int p = threadIdx.x; p < L; p += kGenBlock) {
+        const int f = p / N, n = p - f * N;
+        b0[p] = f < nf ? frame_sample(a.src, N, f0 + f, n) : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    const float2* X = gen_engine(b0, b1, N, B, a.rl, a.tw);
+    if (a.store_mode == 0) {
+        // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o
+        const int sh = N - N / 2;
+        for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
+            const int f = p / N, o = p - f * N;
+            int k = o + sh;
+            if (k >= N) k -= N;
+            const float2 x = X[f * N + k];
+            a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
+        }
+    } else {
+        for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
+            const int f = p / N, k = p - f * N;
+            store_bin(a.out, f0 + f, N, k, X[p], a.store_mode, a.norm);
+        }
+    }
+}
+
+// ---- four-step over two mixed-radix tiles (n = n1 + N1 n2, k = k2 + N2 k1) -------------
+struct Gen4Args {
+    FrameSrc src;
+    long nframes;
+    int N, N1, N2;
+    RadixList rlA, rlB;      // N2-point (pass A) and N1-point (pass B) plans
+    const float2* twA;       // W_N2
+    const float2* twB;       // W_N1
+    const float2* twN;       // W_N
+    float norm;
+    int store_mode;
+    float2* scratch;         // nframes x N: S[f][n1 N2 + k2]
+    float2* out;
+};
+
+__global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
+    extern __shared__ float2 glds[];
+    const int N1 = a.N1, N2 = a.N2;
+    const int C = kGenTile / N2;
+    const int tiles = (N1 + C - 1) / C;
+    const long f = blockIdx.x / tiles;
+    const int c0 = (int)(blockIdx.x % tiles) * C;
+    if (f >= a.nframes) return;
+    const int nc = min(C, N1 - c0);
+    float2* b0 = glds;
+    float2* b1 = glds + nc * N2;
+    // rows of nc contiguous samples (lanes walk the column)
+    for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
+        const int n2 = p / nc, col = p - n2 * nc;
+        b0[col * N2 + n2] = frame_sample(a.src, a.N, f, (long)(c0 + col) + (long)N1 * n2);
+    }
+    __syncthreads();
+    const float2* X = gen_engine(b0, b1, N2, nc, a.rlA, a.twA);
+    float2* S = a.scratch + f * (long)a.N + (long)c0 * N2;
+    for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
+        const int col = p / N2, k2 = p - col * N2;
+        S[p] = cmul(X[p], a.twN[(c0 + col) * k2]);   // (n1 k2 < N)
+    }
+}
+
+__global__ __launch_bounds__(kGenBlock) void gen4_pass_b(Gen4Args a) {
+    extern __shared__ float2 glds[];
+    const int N1 = a.N1, N2 = a.N2;
+    const int C = kGenTile / N1;
+    const int tiles = (N2 + C - 1) / C;
+    const long f = blockIdx.x / tiles;
+    const int c0 = (int)(blockIdx.x % tiles) * C;
+    if (f >= a.nframes) return;
+    const int nc = min(C, N2 - c0);
+    float2* b0 = glds;
+    float2* b1 = glds + nc * N1;
+    const float2* S = a.scratch + f * (long)a.N;
+    for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
+        const int n1 = p / nc, col = p - n1 * nc;
+        b0[col * N1 + n1] = S[(long)n1 * N2 + c0 + col];
+    }
+    __syncthreads();
+    const float2* X = gen_engine(b0, b1, N1, nc, a.rlB, a.twB);
+    for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
+        const int k1 = p / nc, col = p - k1 * nc;
+        const long k = (long)(c0 + col) + (long)N2 * k1;
+        store_bin(a.out, f, a.N, k, X[col * N1 + k1], a.store_mode, a.norm);
+    }
+}
+
+// ---- Bluestein --------------------------------------------------------------------------
+struct BluArgs {
+    FrameSrc src;
+    long nframes;
+    int N, M;
+    const float2* chirp;  // w[n] = e^{-i pi n^2 / N}, N entries
+    const float2* bhat;   // conj(FFT_M(b)) / M ... see blu_mid
+    float2* T;            // nframes x M work frames
+    float norm;
+    int store_mode;
+    float2* out;
+};
+
+__global__ void blu_pre(BluArgs a) {
+    const long total = a.nframes * (long)a.M;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+         i += (long)gridDim.x * blockDim.x) {
+        const long f = i / a.M;
+        const int m = (int)(i - f * a.M);
+        a.T[i] = m < a.N ? cmul(frame_sample(a.src, a.N, f, m), a.chirp[m]) : make_float2(0.f, 0.f);
+    }
+}
+
+// T = conj(FFT(a) * Bh) with Bh = FFT_M(b) / M: the next forward transform then gives
+// conj(M * IFFT(FFT(a) Bh)) = conj(a (*) b) (circular convolution of length M)
+__global__ void blu_mid(BluArgs a) {
+    const long total = a.nframes * (long)a.M;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+         i += (long)gridDim.x * blockDim.x) {
+        const int m = (int)(i % a.M);
+        a.T[i] = conjf2(cmul(a.T[i], a.bhat[m]));
+    }
+}
+
+__global__ void blu_post(BluArgs a) {
+    const long total = a.nframes * (long)a.N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+         i += (long)gridDim.x * blockDim.x) {
+        const long f = i / a.N;
+        const int k = (int)(i - f * a.N);
+        const float2 c = conjf2(a.T[f * a.M + k]);
+        store_bin(a.out, f, a.N, k, cmul(a.chirp[k], c), a.store_mode, a.norm);
+    }
+}
+
+// ---- host side ----------------------------------------------------------------------------
+bool radices(int n, RadixList& rl) {
+    rl.n = 0;
+    int twos = 0;
+    while (n % 2 == 0) {
+        n /= 2;
+        ++twos;
+    }
+    while (twos >= 4) {
+        rl.R[rl.n++] = 16;
+        twos -= 4;
+    }
+    if (twos) rl.R[rl.n++] = 1 << twos;
+    for (int p : {3, 5, 7, 11, 13}) {
+        while (n % p == 0) {
+            if (rl.n >= kMaxPass) return false;
+            rl.R[rl.n++] = p;
+            n /= p;
+        }
+    }
+    return n == 1;
+}
+
+std::vector<float2> twiddles(long n) {
+    std::vector<float2> t((size_t)n);
+    for (long m = 0; m < n; ++m) {
+        const double ang = -2.0 * M_PI * (double)m / (double)n;
+        t[(size_t)m] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+    }
+    return t;
+}
+
+// in-place iterative radix-2 forward DFT in f64 (host, plan time only)
+void host_fft(std::vector<std::complex<double>>& a) {
+    const size_t n = a.size();
+    for (size_t i = 1, j = 0; i < n; ++i) {
+        size_t bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(a[i], a[j]);
+    }
+    for (size_t len = 2; len <= n; len <<= 1) {
+        const double ang = -2.0 * M_PI / (double)len;
+        for (size_t i = 0; i < n; i += len)
+            for (size_t k = 0; k < len / 2; ++k) {
+                const std::complex<double> w(std::cos(ang * k), std::sin(ang * k));
+                const auto u = a[i + k], v = a[i + k + len / 2] * w;
+                a[i + k] = u + v;
+                a[i + k + len / 2] = u - v;
+            }
+    }
+}
+
+template <typename T>
+bool upload(T** d, const std::vector<T>& h) {
+    return hipMalloc(d, h.size() * sizeof(T)) == hipSuccess &&
+           hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+enum { kTileKind = 1, kFourKind = 2, kBluKind = 3 };
+
+}  // namespace
+
+struct GenFftPlan {
+    int N = 0, kind = 0;
+    float norm = 1.f;
+    RadixList rl, rlA, rlB;
+    int N1 = 0, N2 = 0;
+    float2 *tw = nullptr, *twA = nullptr, *twB = nullptr;
+    int M = 0;
+    void* inner = nullptr;  // power-of-two plan of size M (Bluestein)
+    float2 *chirp = nullptr, *bhat = nullptr;
+};
+
+void fftgen_plan_destroy(void* plan) {
+    auto* p = static_cast<GenFftPlan*>(plan);
+    if (!p) return;
+    for (float2* q : {p->tw, p->twA, p->twB, p->chirp, p->bhat})
+        if (q) (void)hipFree(q);
+    if (p->inner) fft_plan_destroy(p->inner);
+    delete p;
+}
+
+void* fftgen_plan_create(int N, int* status) {
+    auto* p = new GenFftPlan();
+    p->N = N;
+    p->norm = 1.0f / sqrtf((float)N);  // f32, like fft.rs:16
+    bool ok = true;
+    RadixList rl;
+    const bool smooth = radices(N, rl);
+    if (smooth && N <= kGenTile) {
+        p->kind = kTileKind;
+        p->rl = rl;
+        ok = upload(&p->tw, twiddles(N));
+    } else if (smooth) {
+        int d = (int)std::sqrt((double)N);
+        while (d > 1 && (N % d || N / d > kGenTile)) --d;
+        RadixList a, b;
+        if (d > 1 && N % d == 0 && N / d <= kGenTile && radices(d, a) && radices(N / d, b)) {
+            p->kind = kFourKind;
+            p->N2 = d;
+            p->N1 = N / d;
+            p->rlA = a;
+            p->rlB = b;
+            ok = upload(&p->tw, twiddles(N)) && upload(&p->twA, twiddles(p->N2)) &&
+                 upload(&p->twB, twiddles(p->N1));
+        }
+    }
+    if (!p->kind) {
+        // Bluestein with a power-of-two convolution length M >= 2N - 1 (fft.hip: M <= 2^20)
+        long M = 1;
+        while (M < 2L * N - 1) M <<= 1;
+        if (M > (1L << 20)) {
+            delete p;
+            *status = SDRGPU_ERR_UNSUPPORTED;
+            return nullptr;
+        }
+        p->kind = kBluKind;
+        p->M = (int)M;
+        std::vector<float2> w((size_t)N);
+        std::vector<std::complex<double>> b((size_t)M, 0.0);
+        for (long n = 0; n < N; ++n) {
+            const long q = (long)((unsigned long long)n * (unsigned long long)n % (2ULL * N));
+            const double ang = -M_PI * (double)q / (double)N;
+            const std::complex<double> wn(std::cos(ang), std::sin(ang));
+            w[(size_t)n] = make_float2((float)wn.real(), (float)wn.imag());
+            b[(size_t)n] = std::conj(wn);
+            if (n) b[(size_t)(M - n)] = std::conj(wn);
+        }
+        host_fft(b);
+        std::vector<float2> bh((size_t)M);
+        for (long m = 0; m < M; ++m)
+            bh[(size_t)m] = make_float2((float)(b[(size_t)m].real() / M), (float)(b[(size_t)m].imag() / M));
+        int st = SDRGPU_OK;
+        p->inner = fft_plan_create((int)M, &st);
+        ok = st == SDRGPU_OK && upload(&p->chirp, w) && upload(&p->bhat, bh);
+    }
+    if (!ok) {
+        fftgen_plan_destroy(p);
+        *status = SDRGPU_ERR_NOMEM;
+        return nullptr;
+    }
+    *status = SDRGPU_OK;
+    return p;
+}
+
+size_t fftgen_frame_scratch_bytes(void* plan) {
+    auto* p = static_cast<GenFftPlan*>(plan);
+    if (p->kind == kFourKind) return (size_t)p->N * sizeof(float2);
+    if (p->kind == kBluKind)
+        return (size_t)p->M * sizeof(float2) * (fft_scratch_frames(p->inner) ? 2 : 1);
+    return 0;
+}
+
+int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
+                  size_t scratch_frames, hipStream_t s) {
+    auto* p = static_cast<GenFftPlan*>(plan);
+    if (fr.nframes <= 0) return SDRGPU_OK;
+    FrameSrc src;
+    src.mode = fr.mode;
+    src.in = fr.in;
+    src.in_real = fr.in_real;
+    src.n_in = fr.n_in;
+    src.hist = fr.hist;
+    src.H = fr.H;
+    src.first_end = fr.first_end;
+    src.hop = fr.hop;
+    const long N = p->N;
+    const long ostride = store_mode == 1 ? N - N / 2 : N;
+    auto advance = [&](FrameSrc& a, long f0) {
+        if (a.mode == 1) a.first_end += f0 * a.hop;
+        else if (a.mode == 0) a.in += f0 * N;
+        else a.in_real += f0 * N;
+    };
+    if (p->kind == kTileKind) {
+        GenTileArgs a{};
+        a.src = src;
+        a.nframes = fr.nframes;
+        a.N = (int)N;
+        a.B = std::max(1, kGenTile / (int)N);
+        a.rl = p->rl;
+        a.tw = p->tw;
+        a.norm = p->norm;
+        a.store_mode = store_mode;
+        a.out = out;
+        const long blocks = (fr.nframes + a.B - 1) / a.B;
+        hipLaunchKernelGGL(gen_tile_kernel, dim3((unsigned)blocks), dim3(kGenBlock),
+                           2 * (size_t)a.B * N * sizeof(float2), s, a);
+        SDRGPU_LAUNCH_CHECK();
+        return SDRGPU_OK;
+    }
+    if (!scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
+    if (p->kind == kFourKind) {
+        Gen4Args a{};
+        a.N = (int)N;
+        a.N1 = p->N1;
+        a.N2 = p->N2;
+        a.rlA = p->rlA;
+        a.rlB = p->rlB;
+        a.twA = p->twA;
+        a.twB = p->twB;
+        a.twN = p->tw;
+        a.norm = p->norm;
+        a.store_mode = store_mode;
+        a.scratch = scratch;
+        const int CA = kGenTile / p->N2, CB = kGenTile / p->N1;
+        const long ta = (p->N1 + CA - 1) / CA, tb = (p->N2 + CB - 1) / CB;
+        for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
+            const long nf = std::min((long)scratch_frames, fr.nframes - f0);
+            a.src = src;
+            advance(a.src, f0);
+            a.nframes = nf;
+            a.out = out + f0 * ostride;
+            hipLaunchKernelGGL(gen4_pass_a, dim3((unsigned)(nf * ta)), dim3(kGenBlock),
+                               2 * (size_t)std::min(CA, p->N1) * p->N2 * sizeof(float2), s, a);
+            SDRGPU_LAUNCH_CHECK();
+            hipLaunchKernelGGL(gen4_pass_b, dim3((unsigned)(nf * tb)), dim3(kGenBlock),
+                               2 * (size_t)std::min(CB, p->N2) * p->N1 * sizeof(float2), s, a);
+            SDRGPU_LAUNCH_CHECK();
+        }
+        return SDRGPU_OK;
+    }
+    // Bluestein: per batch, T (nf x M) then (if the inner plan needs one) its own scratch
+    const long M = p->M;
+    const bool inner_scratch = fft_scratch_frames(p->inner) != 0;
+    float2* inner_buf = inner_scratch ? scratch + (long)scratch_frames * M : nullptr;
+    BluArgs a{};
+    a.N = (int)N;
+    a.M = (int)M;
+    a.chirp = p->chirp;
+    a.bhat = p->bhat;
+    a.T = scratch;
+    a.norm = p->norm;
+    a.store_mode = store_mode;
+    for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
+        const long nf = std::min((long)scratch_frames, fr.nframes - f0);
+        a.src = src;
+        advance(a.src, f0);
+        a.nframes = nf;
+        a.out = out + f0 * ostride;
+        const unsigned g = (unsigned)std::min<long>(4096, (nf * M + 255) / 256);
+        hipLaunchKernelGGL(blu_pre, dim3(g), dim3(256), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+        FftFrames in{};
+        in.mode = 0;
+        in.in = scratch;
+        in.nframes = nf;
+        int st = fft_launch(p->inner, in, scratch, 2, inner_buf, inner_scratch ? scratch_frames : 0, s);
+        if (st) return st;
+        hipLaunchKernelGGL(blu_mid, dim3(g), dim3(256), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+        if ((st = fft_launch(p->inner, in, scratch, 2, inner_buf, inner_scratch ? scratch_frames : 0, s)))
+            return st;
+        const unsigned gp = (unsigned)std::min<long>(4096, (nf * N + 255) / 256);
+        hipLaunchKernelGGL(blu_post, dim3(gp), dim3(256), 0, s, a);
+        SDRGPU_LAUNCH_CHECK();
+    }
+    return SDRGPU_OK;
+}
+
+}  // namespace sdrgpu

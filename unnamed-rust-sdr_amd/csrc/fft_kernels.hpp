@@ -21,10 +21,18 @@ struct FftFrames {
 void* fft_plan_create(int M, int* status);
 void fft_plan_destroy(void* plan);
 int fft_plan_size(void* plan);
-size_t fft_scratch_frames(void* plan);  // 0 if no scratch is needed
-// store_mode 0: collated fft (fft.rs:14-26); 1: rfft upper half (fft.rs:35)
+size_t fft_scratch_frames(void* plan);  // frames per batch; 0 if no scratch is needed
+size_t fft_scratch_bytes(void* plan);   // scratch slab bytes for one batch
+// store_mode 0: collated fft (fft.rs:14-26); 1: rfft upper half (fft.rs:35); 2: natural
+// order, unscaled (internal)
 int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
                size_t scratch_frames, hipStream_t s);
+// sizes that are not powers of two (fft_gen.hip)
+void* fftgen_plan_create(int N, int* status);
+void fftgen_plan_destroy(void* plan);
+size_t fftgen_frame_scratch_bytes(void* plan);
+int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
+                  size_t scratch_frames, hipStream_t s);
 int stft_carry_launch(const float2* in, long n_in, const float2* hist, float2* hist_next, long H,
                       hipStream_t s);
 

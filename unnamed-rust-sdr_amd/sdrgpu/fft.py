@@ -6,8 +6,8 @@
 `fft(x, rate)` / `rfft(x, rate)` return (freqs, values) arrays instead of a Vec of tuples;
 values are the collated, 1/sqrt(N)-normalised spectrum exactly as the reference orders it.
 `Stft` is the streaming composition sig.window(N/rate).decimate(rate/hop).map(fft::fft)
-(examples/live.rs:29-39).  N must be a power of two (rustfft accepts any N: other sizes
-raise SdrGpuError(ERR_UNSUPPORTED)).
+(examples/live.rs:29-39).  Any N >= 1 plans, like rustfft (fft.rs:10-11): powers of two on
+the Stockham / four-step kernels, other lengths on mixed-radix tiles or Bluestein.
 """
 from __future__ import annotations
 
@@ -62,11 +62,12 @@ class FftPlan:
         return out[0] if squeeze else out
 
     def exec_real(self, x) -> np.ndarray:
-        """rfft frames: (count, n) real -> (count, n/2) bins [n/2, n) of the collated output."""
+        """rfft frames: (count, n) real -> (count, n - n/2) entries [n/2, n) of the collated
+        output (fft.rs:35 drains the first n/2)."""
         x = np.ascontiguousarray(x, np.float32)
         squeeze = x.ndim == 1
         x2 = x.reshape(-1, self.n)
-        out = np.empty((x2.shape[0], self.n // 2), np.complex64)
+        out = np.empty((x2.shape[0], self.n - self.n // 2), np.complex64)
         check(lib().sdrgpu_rfft_exec(self._h, x2.ctypes.data, out.ctypes.data, x2.shape[0]),
               "sdrgpu_rfft_exec")
         return out[0] if squeeze else out
