@@ -184,11 +184,7 @@ int dispatch_direct(const FirParams& p, hipStream_t s) {
 }  // namespace
 
 int fir_direct_launch(const FirParams& p, hipStream_t s) {
-    static const bool v1_only = [] {
-        const char* e = getenv("SDRGPU_DIRECT_V1");
-        return e && atoi(e) != 0;
-    }();
-    if (!v1_only && !p.force_naive && fir_direct2_supported(p)) return fir_direct2_launch(p, s);
+    if (!p.force_naive && fir_direct2_supported(p)) return fir_direct2_launch(p, s);
     if (p.sample_kind == SDRGPU_F32 && p.tap_kind == SDRGPU_F32)
         return dispatch_direct<float, float>(p, s);
     if (p.sample_kind == SDRGPU_C64 && p.tap_kind == SDRGPU_F32)

@@ -206,184 +206,6 @@ __host__ __device__ constexpr int d3pad(int s) {
 struct __attribute__((aligned(8))) f4u { float a, b, c, d; };  // 8-B aligned 16-B access (dwordx4)
 
 template <int D, int NL>
-__global__ __launch_bounds__(kD2Block, 2) void fir_direct3_kernel(FirParams p, long ntiles,
-                                                                  int wave_lds) {
-    constexpr int R = D3Geom<D>::R, C = D3Geom<D>::C, G4 = D / 2;  // b128 reads per group
-    extern __shared__ __align__(16) unsigned char smem_raw[];
-    using cfloat = const __attribute__((address_space(4))) float;
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    float2* const wl = reinterpret_cast<float2*>(smem_raw) + wave * wave_lds;
-
-    const long ch = blockIdx.y;
-    const float2* __restrict__ in = static_cast<const float2*>(p.in) + ch * p.ld_in;
-    const float2* __restrict__ hist = static_cast<const float2*>(p.hist) + ch * (long)(p.K - 1);
-    float2* __restrict__ out = static_cast<float2*>(p.out) + ch * p.ld_out;
-    cfloat* taps = (cfloat*)(p.taps_pm);
-    const int K = p.K;
-    const int tpp = p.tpp;
-    const int H = D * tpp;  // multiple of 32
-    const int nchunk = tpp / C;
-    constexpr long TO = 64L * R;
-
-    // staging: lane holds samples 2*lane + 128 i (+1), i < NL  (NL*128 >= H + 2048)
-    float4 st[NL];
-    auto tile_s0 = [&](long tile) { return p.i0 + tile * TO * D - H; };
-    auto interior = [&](long s0) { return s0 >= 0 && s0 + 128L * NL <= p.n_in; };
-    auto load_tile = [&](long tile) {
-        const long s0 = tile_s0(tile);
-        if (interior(s0)) {
-            const f4u* src = reinterpret_cast<const f4u*>(in + s0 + 2 * lane);
-#pragma unroll
-            for (int i = 0; i < NL; ++i) {
-                const f4u v = src[64 * i];
-                st[i] = make_float4(v.a, v.b, v.c, v.d);
-            }
-        }
-    };
-
-    long tile = (long)blockIdx.x * (kD2Block / 64) + wave;
-    const long tstride = (long)gridDim.x * (kD2Block / 64);
-    if (tile < ntiles) load_tile(tile);
-
-    const int wbase = d3pad(H) + 34 * lane;       // padded H + 32*lane
-    const int sbase = 2 * lane + 2 * (lane / 16);  // padded 2*lane
-
-#pragma unroll 1
-    for (; tile < ntiles; tile += tstride) {
-        {
-            const long s0 = tile_s0(tile);
-            if (interior(s0)) {
-#pragma unroll
-                for (int i = 0; i < NL; ++i)
-                    *reinterpret_cast<float4*>(wl + sbase + 136 * i) = st[i];  // d3pad(128 i) = 136 i
-            } else {
-#pragma unroll 1
-                for (int i = 0; i < NL; ++i) {
-                    const long g = s0 + 2 * lane + 128 * i;
-                    const float2 a = fetch_c64(in, p.n_in, hist, K, g);
-                    const float2 b = fetch_c64(in, p.n_in, hist, K, g + 1);
-                    *reinterpret_cast<float4*>(wl + sbase + 136 * i) = make_float4(a.x, a.y, b.x, b.y);
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        if (tile + tstride < ntiles) load_tile(tile + tstride);
-
-        float2 acc[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) acc[j] = make_float2(0.f, 0.f);
-
-        const float2* const lb = wl + wbase;
-        // group q (chunk-relative) -> D samples; grp[i][r] = sample D*(-i) + r, i = 0..C
-        auto read_group = [&](const float2* lc, int q, float2* g) {
-#pragma unroll
-            for (int h2 = 0; h2 < G4; ++h2) {
-                typedef float v4f __attribute__((ext_vector_type(4)));
-                v4f v = *reinterpret_cast<const v4f*>(lc + d3pad(D * q) + 2 * h2);
-                g[2 * h2] = make_float2(v.x, v.y);
-                g[2 * h2 + 1] = make_float2(v.z, v.w);
-            }
-        };
-        // carried state: cur[p][e-1] = X_p[e], e = 1..R-1; g0 = group 0 (X_0[0], X_p[1])
-        float2 cur[D][R - 1];
-        float2 g0[D];
-        {
-            float2 gq[D];
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                read_group(lb, q, gq);
-                if (q == 0) {
-#pragma unroll
-                    for (int r = 0; r < D; ++r) g0[r] = gq[r];
-                }
-                // X_0[q] (q >= 1) and X_{D-r}[q+1] (q+1 <= R-1)
-                if (q >= 1) cur[0][q - 1] = gq[0];
-#pragma unroll
-                for (int r = 1; r < D; ++r)
-                    if (q + 1 <= R - 1) cur[D - r][q] = gq[r];
-            }
-            // X_{D-r}[1] comes from group 0
-#pragma unroll
-            for (int r = 1; r < D; ++r) cur[D - r][0] = g0[r];
-        }
-
-#pragma unroll 1
-        for (int c = 0; c < nchunk; ++c) {
-            // chunk shift: C taps = D*C = 32 samples = 34 padded slots per chunk
-            const float2* lc = lb - 34 * c;
-            float2 gn[C][D];  // gn[i-1] = group -i, i = 1..C
-#pragma unroll
-            for (int i = 1; i <= C; ++i) read_group(lc, -i, gn[i - 1]);
-            // X_p[e] for e in [-(C-1), R-1]
-            auto X = [&](int ph, int e) -> float2 {
-                if (e >= 1) return cur[ph][e - 1];
-                if (ph == 0) return e == 0 ? g0[0] : gn[-e - 1][0];
-                return gn[-e][D - ph];  // group e-1 = -(1-e)
-            };
-#pragma unroll
-            for (int ph = 0; ph < D; ++ph) {
-                cfloat* hc = taps + ph * tpp + c * C;
-#pragma unroll
-                for (int a = 0; a < C; ++a) {
-                    const float h = hc[a];
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        const float2 x = X(ph, j - a);
-                        acc[j].x = fmaf(x.x, h, acc[j].x);
-                        acc[j].y = fmaf(x.y, h, acc[j].y);
-                    }
-                }
-            }
-            // carry to the next chunk (e'' = e + C)
-            float2 ncur[D][R - 1];
-#pragma unroll
-            for (int ph = 0; ph < D; ++ph)
-#pragma unroll
-                for (int e2 = 1; e2 < R; ++e2) ncur[ph][e2 - 1] = X(ph, e2 - C);
-#pragma unroll
-            for (int ph = 0; ph < D; ++ph)
-#pragma unroll
-                for (int e2 = 0; e2 < R - 1; ++e2) cur[ph][e2] = ncur[ph][e2];
-#pragma unroll
-            for (int r = 0; r < D; ++r) g0[r] = gn[C - 1][r];
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-
-        const long m = tile * TO + (long)R * lane;
-        float2* o = out + m;
-        if (m + R <= p.n_out) {
-#pragma unroll
-            for (int j = 0; j < R; j += 2)
-                *reinterpret_cast<f4u*>(o + j) = f4u{acc[j].x, acc[j].y, acc[j + 1].x, acc[j + 1].y};
-        } else {
-#pragma unroll
-            for (int j = 0; j < R; ++j)
-                if (m + j < p.n_out) o[j] = acc[j];
-        }
-    }
-
-    if (blockIdx.x == gridDim.x - 1) {
-        float2* hn = static_cast<float2*>(p.hist_next) + ch * (long)(K - 1);
-        for (int jj = threadIdx.x; jj < K - 1; jj += kD2Block) {
-            const long g = p.n_in - (long)(K - 1) + jj;
-            hn[jj] = g >= 0 ? in[g] : hist[g + (K - 1)];
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------
-// v4: v3's grouped reads, split into D/2 passes (one per 16-B half of a group: samples
-// r = 2h, 2h+1 -> two phases) and software-pipelined with two half-group buffers.  For
-// chunk c the "cur" buffer holds half-groups -(s+1) and the "prev" buffer half-groups
-// C-1-s (chunk-relative, slot s).  Slot s of prev is last read at tap step a = s, so
-// right after step s the half-group chunk c+1 needs in its cur slot s is loaded into it:
-// every LDS read has a whole chunk of FMAs to land, the buffers swap roles without
-// register moves, and they cost 2*C*2 float2 (64 VGPRs at D = 4) next to the staging.
-template <int D, int NL>
 __global__ __launch_bounds__(kD2Block, 2) void fir_direct4_kernel(FirParams p, long ntiles,
                                                                   int wave_lds) {
     constexpr int R = D3Geom<D>::R, C = D3Geom<D>::C, G4 = D / 2;
@@ -554,14 +376,6 @@ inline int cu_count() {
     return n_cu;
 }
 
-int direct_variant() {
-    static const int v = [] {
-        const char* e = getenv("SDRGPU_DIRECT_VARIANT");
-        return e ? atoi(e) : 4;
-    }();
-    return v;
-}
-
 template <int D, int NL>
 int launch_d3(const FirParams& p, hipStream_t s) {
     const int wave_lds = d3pad(128 * NL) + 2;  // elements (even -> 16-B multiple)
@@ -573,12 +387,8 @@ int launch_d3(const FirParams& p, hipStream_t s) {
     if (cap < 1) cap = 1;
     const long gx = std::max(1L, std::min(want, cap));
     dim3 grid((unsigned)gx, (unsigned)p.nch);
-    if (direct_variant() == 3)
-        hipLaunchKernelGGL((fir_direct3_kernel<D, NL>), grid, dim3(kD2Block), lds, s, p, ntiles,
-                           wave_lds);
-    else
-        hipLaunchKernelGGL((fir_direct4_kernel<D, NL>), grid, dim3(kD2Block), lds, s, p, ntiles,
-                           wave_lds);
+    hipLaunchKernelGGL((fir_direct4_kernel<D, NL>), grid, dim3(kD2Block), lds, s, p, ntiles,
+                       wave_lds);
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }
@@ -643,12 +453,11 @@ bool fir_direct2_supported(const FirParams& p) {
 
 int fir_direct2_launch(const FirParams& p, hipStream_t s) {
     if (!fir_direct2_supported(p)) return SDRGPU_ERR_UNSUPPORTED;
-    const bool v2 = direct_variant() == 2;
     switch (p.D) {
     case 1: return dispatch_d2<1>(p, s);
-    case 2: return v2 ? dispatch_d2<2>(p, s) : dispatch_d3<2>(p, s);
-    case 4: return v2 ? dispatch_d2<4>(p, s) : dispatch_d3<4>(p, s);
-    case 8: return v2 ? dispatch_d2<8>(p, s) : dispatch_d3<8>(p, s);
+    case 2: return dispatch_d3<2>(p, s);
+    case 4: return dispatch_d3<4>(p, s);
+    case 8: return dispatch_d3<8>(p, s);
     default: return SDRGPU_ERR_UNSUPPORTED;
     }
 }

@@ -85,8 +85,7 @@ __device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, f32x4 c) {
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// ABL (debug ablation, results invalid): 1 = memory only (no MFMA), 2 = no HBM loads
-template <int D, int NCH, int ABL = 0>
+template <int D, int NCH>
 __global__ __launch_bounds__(kMxBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void fir_mx_kernel(MxParams p) {
     constexpr int NC = D / 2;         // new 32-sample chunks per step
@@ -151,11 +150,6 @@ void fir_mx_kernel(MxParams p) {
     }
 
     auto load_step = [&](float4 (&dst)[NP], long s) {
-        if (ABL == 2) {
-#pragma unroll
-            for (int q = 0; q < NP; ++q) dst[q] = make_float4((float)(s + q), 1.f, 2.f, (float)lane);
-            return;
-        }
         const bool ok = (s >= 0) & (s + 32 * (NC - 1) + 26 <= n_in);
         if (__all(ok)) {
 #pragma unroll
@@ -221,14 +215,7 @@ void fir_mx_kernel(MxParams p) {
             // ---- prefetch the samples of iteration it + NACC into the freed buffer ----
             if (it + NACC < p.n_iter) load_step(raw[r], s0 + hop * (it + NACC));
 
-            if (ABL == 1) {
-                // memory-only ablation: fold the samples into the accumulator lanes
-#pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    accr[(r + 1) % NACC] += __builtin_bit_cast(f32x4, xh[c][0]);
-                    acci[(r + 1) % NACC] += __builtin_bit_cast(f32x4, xh[c][1]);
-                }
-            } else {
+            {
                 // ---- multiply the new chunks into the NACC pending steps ----
 #pragma unroll
                 for (int d = 0; d < NACC; ++d) {
@@ -284,7 +271,7 @@ void fir_mx_kernel(MxParams p) {
 struct MxState {
     int K = 0, D = 0, NCH = 0;
     float* d_taps = nullptr;
-    void* d_dummy = nullptr;  // zeroed target of fir_mxl's clamped prefetches
+    void* d_dummy = nullptr;  // zeroed target of fir_mxh's clamped prefetches
     int tap_scale_exp = 0;    // fir_mxh: 15 - exponent(max |h|)
     int cus = 256;
 };
@@ -332,8 +319,8 @@ void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status) {
         st->cus = cus;
     if (hipMalloc(&st->d_taps, sizeof(float) * K) != hipSuccess ||
         hipMemcpy(st->d_taps, taps, sizeof(float) * K, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc(&st->d_dummy, fir_mxl_dummy_bytes()) != hipSuccess ||
-        hipMemset(st->d_dummy, 0, fir_mxl_dummy_bytes()) != hipSuccess) {
+        hipMalloc(&st->d_dummy, fir_mxh_dummy_bytes()) != hipSuccess ||
+        hipMemset(st->d_dummy, 0, fir_mxh_dummy_bytes()) != hipSuccess) {
         if (st->d_taps) (void)hipFree(st->d_taps);
         if (st->d_dummy) (void)hipFree(st->d_dummy);
         delete st;
@@ -361,17 +348,10 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
         fp.K != st->K)
         return SDRGPU_ERR_UNSUPPORTED;
-    // D = 4: the LDS-staged kernels -- fp16 two-way split at two waves per SIMD
-    // (fir_mxh.hip, default), bf16 three-way split at one (fir_mxl.hip, K <= 385 and
-    // SDRGPU_MX_VARIANT=2); SDRGPU_MX_VARIANT=1 keeps the register-fed kernel below.
-    static const int variant = [] {
-        const char* e = getenv("SDRGPU_MX_VARIANT");
-        return e ? atoi(e) : 3;
-    }();
-    if (variant == 3 && fir_mxh_supported(fp))
+    // D = 4 and D = 1: the LDS-staged fp16 two-way split at two waves per SIMD (fir_mxh.hip);
+    // D = 2 / 8: the register-fed exact bf16 three-way split below
+    if (fir_mxh_supported(fp))
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
-    if (variant >= 2 && fir_mxl_supported(fp))
-        return fir_mxl_launch(fp, st->d_taps, st->d_dummy, st->cus, s);
     if (st->NCH == 0) return SDRGPU_ERR_UNSUPPORTED;  // shape only the fp16 kernel covers
     // 16-byte loads of sample pairs: channel bases must stay 16-byte aligned
     if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
@@ -403,13 +383,9 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     p.n_iter = fp.n_out > 0 ? (int)(ceil_div(steps + NACC - 1, NACC) * NACC) : 0;
     const long waves = ceil_div(p.nseg, 16);
     dim3 grid((unsigned)std::max(1L, ceil_div(waves, kMxBlock / 64)));
-    static const char* abl_env = getenv("SDRGPU_MX_ABLATION");
-    const int abl = abl_env ? atoi(abl_env) : 0;
 #define SDRGPU_MX_CASE(DD, CC)                                                                   \
     if (D == DD && NCH == CC) {                                                                  \
-        if (abl == 1) hipLaunchKernelGGL((fir_mx_kernel<DD, CC, 1>), grid, dim3(kMxBlock), 0, s, p); \
-        else if (abl == 2) hipLaunchKernelGGL((fir_mx_kernel<DD, CC, 2>), grid, dim3(kMxBlock), 0, s, p); \
-        else hipLaunchKernelGGL((fir_mx_kernel<DD, CC, 0>), grid, dim3(kMxBlock), 0, s, p);        \
+        hipLaunchKernelGGL((fir_mx_kernel<DD, CC>), grid, dim3(kMxBlock), 0, s, p);                \
         SDRGPU_LAUNCH_CHECK();                                                                   \
         return SDRGPU_OK;                                                                        \
     }
