@@ -6,6 +6,8 @@ with the same rules (inputs resident in HBM, HIP-event-timed kernels on the hand
 stream, algorithmic bytes per input sample, a bounded CPU-baseline sample), one JSON line
 per config:
 
+  c1  127-tap real FIR over 2^20 f32 (configs[0], the reference CPU path): oracle on 1
+      host core, the same block on the GPU beside it
   c3  64k-point STFT, 50 % overlap, 2^28 c64 samples      24 B / input sample, HBM roof
   c4  255-tap matched filter (FIR bank) + PLL FM demod,    12 B / input sample (+1 lock);
       1024 channels x 2^20 c64                              PLL = loop-carried latency
@@ -38,7 +40,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "all"])
+    ap.add_argument("--config", default="all", choices=["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -83,6 +85,55 @@ def roof(bytes_per_unit, units, ms):
     gbs = bytes_per_unit * units / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_GBS, 4), "kernel_ms": round(ms, 4)}
+
+
+# ------------------------------------------------------------------------------ c1
+def bench_c1(args):
+    """configs[0]: the reference's CPU path -- a 127-tap real lowpass FIR over 2^20 f32
+    samples (examples/filter.rs's signal.filter(...) shape with FIR taps) -- timed as the
+    oracle restatement on one host core; the same block on the GPU beside it."""
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from bench import host_info
+    n = 1 << 20
+    taps = ss.firwin(127, 0.2).astype(np.float32)
+    x = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+    o = pyoracle.Fir(taps, 1, sample_kind=0)
+    t0, done = time.perf_counter(), 0
+    while True:
+        ref = o.process(x)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    fir = sdrgpu.filter.Fir(taps, sample_kind=sdrgpu.F32).design(44100.0)
+    dx = DeviceBuffer.from_numpy(x)
+    dy = DeviceBuffer.empty(n, np.float32)
+
+    def step():
+        assert fir.process_dev(dx.ptr, n, dy.ptr, n) == n
+
+    wall, ms = time_events(step, fir.stream(), args.steps, args.warmup,
+                           lambda: (fir.sync(), synchronize()))
+    # parity of the last GPU block: its FIR history is the block's own tail (steady state)
+    y = dy.download(dtype=np.float32)
+    prev = o.process(x)  # the oracle continues its own stream over the same block
+    err = float(np.abs(y - prev).max() / np.sqrt(np.mean(prev.astype(np.float64) ** 2)))
+    assert err <= 1e-5, err
+    return {"config": "c1: 127-tap real FIR (firwin 0.2), 2^20 f32 samples -- configs[0], "
+                      "the reference CPU path",
+            "metric": "Msamples/s (f32 input)",
+            "cpu_baseline": {"value": round(done / el / 1e6, 2), "unit": "Msamples/s", "cores": 1,
+                             "kind": "port", "host": host_info(),
+                             "sample": f"{done // n} passes of 2^20 f32 samples through the "
+                                       f"oracle Fir (127 taps), {el:.1f} s on 1 host core"},
+            "gpu": {"value": round(n / (ms * 1e-3) / 1e6, 1), "kernel_ms": round(ms, 4),
+                    "algorithm": fir.last_algorithm(), "wall_ms_per_step": round(wall * 1e3, 3),
+                    "parity_max_over_rms": err,
+                    "roofline": roof(8, n, ms)}}
 
 
 # ------------------------------------------------------------------------------ c3
@@ -387,9 +438,9 @@ def bench_src(args):
 
 def main():
     args = parse()
-    todo = ["c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src"] if args.config == "all" else [args.config]
+    todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src"] if args.config == "all" else [args.config]
     for c in todo:
-        r = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
+        r = {"c1": bench_c1, "c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
              "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src}[c](args)
         if r is not None:
             print(json.dumps(r), flush=True)

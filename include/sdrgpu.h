@@ -191,6 +191,14 @@ int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t cou
 /* rfft: `count` frames of n F32 samples -> count frames of n - n/2 C64 values: the collated
  * output with its first n/2 entries drained (fft.rs:35), i.e. X[0 .. n - n/2) * 1/sqrt(n). */
 int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count);
+/* Output format of exec / rfft_exec (and the STFT): SDRGPU_FFT_OUT_COMPLEX (default, C64) or
+ * SDRGPU_FFT_OUT_DB -- one f32 per bin, 20*log10(|X * 1/sqrt(n)|): the magnitude-in-dB
+ * conversion every spectrum plot of the reference applies to fft's output
+ * (ComplexSeries with db = true: y.norm(), then 20 * log10, src/plot/complexseries.rs:90-92;
+ * examples/fft.rs:80-100, examples/live.rs), fused into the transform's store (half the
+ * output bytes). */
+enum sdrgpu_fft_output { SDRGPU_FFT_OUT_COMPLEX = 0, SDRGPU_FFT_OUT_DB = 1 };
+int sdrgpu_fft_set_output(sdrgpu_fft* h, int mode);
 int sdrgpu_fft_sync(sdrgpu_fft* h);
 void sdrgpu_fft_destroy(sdrgpu_fft* h);
 int sdrgpu_fft_freqs(size_t n, float rate, float* freqs);
@@ -210,6 +218,15 @@ int sdrgpu_stft_process(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
                         size_t out_cap_frames, size_t* n_frames);
 int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void* d_out,
                             size_t out_cap_frames, size_t* n_frames);
+/* HOST pointers, asynchronous (as sdrgpu_fir_process_async): H2D + frames enqueued on the
+ * handle's stream, the download on a second stream; pinned buffers (sdrgpu_host_alloc), `in`
+ * unchanged and `out` unread until sdrgpu_stft_sync. */
+int sdrgpu_stft_process_async(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
+                              size_t out_cap_frames, size_t* n_frames);
+/* SDRGPU_C64 (default) or SDRGPU_CU8: raw rtl_tcp I/Q bytes as examples/live.rs feeds
+ * rtl.listen() into window(..) (src/rtltcp.rs:156-164 conversion done in the frame load). */
+int sdrgpu_stft_set_input_kind(sdrgpu_stft* h, int sample_kind);
+int sdrgpu_stft_set_output(sdrgpu_stft* h, int mode);  /* sdrgpu_fft_output */
 int sdrgpu_stft_sync(sdrgpu_stft* h);
 int sdrgpu_stft_reset(sdrgpu_stft* h);
 void sdrgpu_stft_destroy(sdrgpu_stft* h);
@@ -262,6 +279,11 @@ int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,
                        float* out, uint8_t* locked, size_t ld_out);
 int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t n,
                            float* d_out, uint8_t* d_locked, size_t ld_out);
+/* HOST pointers, asynchronous: nch x n dense blocks (ld = n) in, out / locked dense; H2D +
+ * PLL on the handle's stream, downloads on a second stream (the Block hand-off in front of
+ * the PLL, src/main.rs:47-49).  Pinned buffers; read outputs after sdrgpu_pll_sync. */
+int sdrgpu_pll_process_async(sdrgpu_pll* h, const void* in, size_t n, float* out,
+                             uint8_t* locked);
 /* Public Pll fields nphase / value (src/filter/pll.rs:20-21) of channel ch. */
 int sdrgpu_pll_state(sdrgpu_pll* h, size_t ch, float* nphase, float* value_re_im);
 int sdrgpu_pll_sync(sdrgpu_pll* h);

@@ -492,6 +492,52 @@ void oracle_freq(float rate, float freq, float phase, size_t n, float* out) {
     }
 }
 
+/* `value.round() as usize` (Rust): round half away from zero, saturating at 0 (and NaN -> 0) */
+static size_t f32_round_usize(float v) {
+    float r = roundf(v);
+    if (!(r > 0.0f)) return 0;
+    if (r >= 18446744073709551616.0f) return (size_t)-1;
+    return (size_t)r;
+}
+
+/* freq_sweep(rate, df, warmup, start..end) (sources.rs:181-194): dfdt = df.powi(2) (negated
+ * for a falling sweep), endt = (end - start) / dfdt, warmupt = warmup ? 1/df : 0, then
+ * FreqSweep::new(rate, start, dfdt, 0.0, warmupt, warmupt + endt, Some(warmupt + endt))
+ * (:129-143) and FreqSweep::next (:146-174).  Writes at most `cap` samples (freq, value) and
+ * returns the sweep's length. */
+size_t oracle_freq_sweep(float rate, float df, int warmup, float start, float end, size_t cap,
+                         float* freqs, float* out) {
+    float dfdt = df * df;
+    if (start > end) dfdt = -dfdt;
+    float endt = (end - start) / dfdt;
+    float warmupt = warmup ? 1.0f / df : 0.0f;
+    float fend_t = warmupt + endt;
+    float dt = 1.0f / rate;
+    float f = start;
+    float nphase = 0.0f / (2.0f * PI_F);
+    size_t fstart = f32_round_usize(warmupt * rate);
+    size_t fend = f32_round_usize(fend_t * rate);
+    size_t length = f32_round_usize(fend_t * rate);
+    size_t total = length;
+    for (size_t i = 0; i < total && i < cap; ++i) {
+        float d = dfdt;
+        if (fstart > 0) {
+            fstart -= 1;
+            d = 0.0f;
+        }
+        if (fend > 0) fend -= 1;
+        else d = 0.0f;
+        f += dt * d;
+        nphase += dt * f;
+        nphase = nphase - truncf(nphase);
+        float ph = 2.0f * PI_F * nphase;
+        freqs[i] = f;
+        out[2 * i] = 1.0f * cosf(ph);
+        out[2 * i + 1] = 1.0f * sinf(ph);
+    }
+    return total;
+}
+
 /* RtlTcpSignal::next (rtltcp.rs:156-164): (v - 128) / 128 */
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
     for (size_t i = 0; i < 2 * n; ++i) out[i] = ((float)in[i] - 128.0f) / 128.0f;

@@ -112,6 +112,10 @@ int  oracle_src_process(oracle_src* s, const float* in, long in_frames, float* o
 /* ---------------- Sources (src/signal/sources.rs) ------------------------------- */
 /* freq(rate, f, phase) (sources.rs:196-221 via FreqSweep::next :150-175), n samples */
 void oracle_freq(float rate, float freq, float phase, size_t n, float* out);
+/* freq_sweep(rate, df, warmup, start..end) (sources.rs:181-194 via FreqSweep, :116-179):
+ * up to cap (freq, value) samples; returns the sweep length */
+size_t oracle_freq_sweep(float rate, float df, int warmup, float start, float end, size_t cap,
+                         float* freqs, float* out);
 /* rtl_tcp u8 IQ -> f32 (src/rtltcp.rs:156-164) */
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out);
 

@@ -62,6 +62,9 @@ def lib():
         L.oracle_stft.argtypes = [c_void_p, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t,
                                   c_int]
         L.oracle_freq.argtypes = [c_float, c_float, c_float, c_size_t, c_void_p]
+        L.oracle_freq_sweep.restype = c_size_t
+        L.oracle_freq_sweep.argtypes = [c_float, c_float, c_int, c_float, c_float, c_size_t,
+                                        c_void_p, c_void_p]
         L.oracle_u8_to_c64.argtypes = [c_void_p, c_size_t, c_void_p]
         L.oracle_src_new.restype = c_void_p
         L.oracle_src_new.argtypes = [c_int, c_int, POINTER(c_int)]
@@ -187,6 +190,15 @@ def freq(rate, f, phase, n):
     out = np.empty(n, np.complex64)
     lib().oracle_freq(rate, f, phase, n, out.ctypes.data)
     return out
+
+
+def freq_sweep(rate, df, warmup, start, end):
+    """(freqs f32, values c64) of freq_sweep(rate, df, warmup, start..end) (sources.rs:181-194)."""
+    n = lib().oracle_freq_sweep(rate, df, int(warmup), start, end, 0, None, None)
+    f = np.empty(n, np.float32)
+    v = np.empty(n, np.complex64)
+    lib().oracle_freq_sweep(rate, df, int(warmup), start, end, n, f.ctypes.data, v.ctypes.data)
+    return f, v
 
 
 def u8_to_c64(iq_u8):

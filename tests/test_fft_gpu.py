@@ -175,3 +175,55 @@ def test_stft_c3_shape_device(sdr, oracle):
     for j in (0, 1, 11, nf - 1):
         ref = oracle.stft(x[:(j + 1) * hop], n, hop)[j]
         assert_parity(y[j], ref, what=f"frame {j}")
+
+
+def _db_ref(c):
+    """src/plot/complexseries.rs:90-92 in float64: 20 * log10(|y|)."""
+    return 20.0 * np.log10(np.abs(c.astype(np.complex128)))
+
+
+@pytest.mark.parametrize("n", [1024, 1000, 65536, 14400])
+def test_fft_db_output(sdr, oracle, n):
+    """The fused |X| -> dB store equals 20 log10 |fft| of the oracle to 1e-4 dB (bins within
+    100 dB of the frame's peak; deeper bins are dominated by f32 rounding either way)."""
+    rng = np.random.default_rng(n)
+    x = cplx(rng, 2 * n).reshape(2, n)
+    y = sdr.fft.FftPlan(n, output="db").exec(x)
+    assert y.dtype == np.float32 and y.shape == (2, n)
+    for c in range(2):
+        ref = _db_ref(oracle.fft_frame(x[c]) if n <= 20000 else
+                      np.fft.fftshift(np.fft.fft(x[c].astype(np.complex128))) / np.sqrt(n))
+        keep = ref > ref.max() - 100
+        assert np.abs(y[c][keep] - ref[keep]).max() < 1e-4
+    r = sdr.fft.FftPlan(n, output="db").exec_real(x.real.astype(np.float32))
+    full = np.fft.fftshift(np.fft.fft(x.real.astype(np.float64), axis=1), axes=1) / np.sqrt(n)
+    ref = _db_ref(full[:, n // 2:])
+    assert r.shape == ref.shape
+    keep = ref > ref.max() - 100
+    assert np.abs(r[keep] - ref[keep]).max() < 1e-4
+
+
+def test_stft_db_output(sdr, oracle):
+    rng = np.random.default_rng(5)
+    n, hop = 65536, 32768
+    x = cplx(rng, hop * 5 + 11)
+    y = sdr.fft.Stft(n, hop, output="db").process(x)
+    ref = oracle.stft(x, n, hop, nthreads=8)
+    assert y.shape == ref.shape and y.dtype == np.float32
+    for j in range(ref.shape[0]):
+        r = _db_ref(ref[j])
+        keep = r > r.max() - 100
+        assert np.abs(y[j][keep] - r[keep]).max() < 1e-4, j
+
+
+def test_stft_u8_input(sdr, oracle):
+    from sdrgpu import _lib
+    rng = np.random.default_rng(6)
+    for n, hop in ((4096, 1000), (65536, 32768)):
+        iq = rng.integers(0, 256, 2 * (hop * 4 + 5), dtype=np.uint8)
+        s = sdr.fft.Stft(n, hop, input_kind=_lib.CU8)
+        y = np.concatenate([s.process(iq[:2 * 777]), s.process(iq[2 * 777:])])
+        ref = oracle.stft(oracle.u8_to_c64(iq), n, hop, nthreads=8)
+        assert y.shape == ref.shape
+        for j in range(ref.shape[0]):
+            assert_parity(y[j], ref[j], what=f"u8 stft n={n} frame {j}")

@@ -131,3 +131,30 @@ def test_oracle_u8_ingest(oracle):
 def test_rms_metric_sanity():
     a = np.ones(10)
     assert rms_rel_err(a, a) == (0.0, 0.0)
+
+
+def test_oracle_freq_sweep_shape(oracle):
+    """freq_sweep(1.8e6, 20e3, warmup, -200e3..200e3) (examples/pll.rs:8-11): 1/df of
+    warmup at the start frequency, then a linear ramp of df^2 Hz/s to the end frequency."""
+    f, v = oracle.freq_sweep(1.8e6, 20000.0, True, -200000.0, 200000.0)
+    n_warm = round(1.8e6 / 20000.0)
+    assert f.size == round((1 / 20000.0 + 400000.0 / 4e8) * 1.8e6)
+    assert np.all(f[:n_warm] == -200000.0)
+    step = np.diff(f[n_warm:])
+    assert np.allclose(step, 4e8 / 1.8e6, rtol=1e-3)
+    assert abs(f[-1] - 200000.0) < 250.0
+    assert np.allclose(np.abs(v), 1.0, atol=1e-6)
+
+
+def test_sweep_mirror_matches_oracle(sdr, oracle):
+    """sdrgpu.signal.freq_sweep (host source of the mirror) = the oracle's, bit for bit."""
+    for args in ((1.8e6, 20000.0, True, -200000.0, 200000.0), (44100.0, 100.0, True, -20000.0, 20000.0),
+                 (48000.0, 500.0, False, 3000.0, -3000.0)):
+        f, v = oracle.freq_sweep(*args)
+        r = sdr.signal.freq_sweep(*args, block=1000).collect()
+        assert np.array_equal(r["freq"], f) and np.array_equal(r["value"], v)
+
+
+def test_freq_mirror_matches_oracle(sdr, oracle):
+    x = sdr.signal.freq(1.8e6, 50e3, 0.3, 5000, block=999).collect()
+    assert np.array_equal(x, oracle.freq(1.8e6, 50e3, 0.3, 5000))

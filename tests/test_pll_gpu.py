@@ -175,3 +175,24 @@ def test_pll_rtl_tcp_u8_input(sdr, oracle):
     ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), xc)
     assert np.array_equal(np.concatenate([out_u8, o2], 1), ref_out)
     assert np.array_equal(np.concatenate([lk_u8, l2], 1), ref_lk)
+
+
+def test_pll_examples_frequency_sweep_kat(sdr, oracle):
+    """examples/pll.rs:8-18: the PLL over freq_sweep(1.8 MHz, df = 20 kHz, warmup,
+    -200 kHz..200 kHz).  Bit-exact to the oracle, and the reference's expected picture: the
+    loop locks over the middle of the sweep and its output tracks the input frequency, delayed
+    by the output filter (LowPass 20 kHz: 24 samples at 4e8 Hz/s)."""
+    rate = 1.8e6
+    f, v = oracle.freq_sweep(rate, 20000.0, True, -200000.0, 200000.0)
+    fl = sdr.filter
+    d = fl.PllDesign(0.0, 0.035, fl.BiquadD.LowPass(80000.0, 0.7), fl.BiquadD.LowPass(20000.0, 0.7),
+                     fl.BiquadD.LowPass(20000.0, 0.7))
+    out, lk = d.design(rate).process(v)
+    ro, rl = oracle.pll_batch(oracle_params(oracle, outf=(1, 20000.0, 0.7)), v)
+    check(out, lk, ro[0], rl[0], "sweep")
+    idx = np.nonzero(lk)[0]
+    assert idx.size == idx[-1] - idx[0] + 1            # one contiguous locked stretch
+    assert f[idx[0]] < -80000.0 and f[idx[-1]] > 80000.0
+    delayed = f[idx - 24]
+    assert np.abs(out[idx] - delayed).max() < 50.0     # out ~ f (24-sample filter delay)
+    assert np.corrcoef(out[idx], f[idx])[0, 1] > 0.9999

@@ -62,3 +62,76 @@ def test_filter_pll(sdr, oracle):
     p = oracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
     ro, rl = oracle.pll_batch(p, x)
     assert np.array_equal(r["value"], ro[0]) and np.array_equal(r["locked"], rl[0].astype(bool))
+
+
+# ---- rtl_tcp byte blocks (CU8): adapters count SAMPLES (byte pairs), never single bytes ----
+def _iq(n, seed=0):
+    return np.random.default_rng(seed).integers(0, 256, 2 * n, dtype=np.uint8)
+
+
+def test_cu8_take_skip_decimate_count_samples(sdr, oracle):
+    from sdrgpu import _lib
+    iq = _iq(1000)
+    s = sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8)
+    got = s.skip(1.5).take(2.0).collect()          # samples 150 .. 350 -> bytes 300 .. 700
+    assert np.array_equal(got, iq[300:700])
+    d = sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8).decimate(25.0).collect()
+    pairs = iq.reshape(-1, 2)[3::4].reshape(-1)      # kept samples wait-1, 2wait-1, ...
+    assert np.array_equal(d, pairs)
+
+
+def test_cu8_window_raw_frames_convert_samples(sdr, oracle):
+    """window(..).decimate(..).map(f) with a non-FFT map sees Complex samples, as
+    RtlTcpSignal::next yields them (src/rtltcp.rs:156-164)."""
+    from sdrgpu import _lib
+    iq = _iq(300, 1)
+    n, hop = 16, 8
+    fr = (sdr.signal.from_array(1.0, iq, block=50, sample_kind=_lib.CU8).window(n / 1.0)
+          .decimate(1.0 / hop).map(lambda f: f).collect())
+    x = oracle.u8_to_c64(iq)
+    assert fr.shape == (300 // hop, n)
+    for j in range(fr.shape[0]):
+        beg = (j + 1) * hop - n
+        want = np.zeros(n, np.complex64)
+        want[max(0, -beg):] = x[max(0, beg):beg + n]
+        assert np.array_equal(fr[j], want)
+
+
+@pytest.mark.gpu
+def test_cu8_filter_then_pll_and_fir_chain(sdr, oracle):
+    """rtl.listen().filter(taps).filter(pll) and a two-FIR chain: the FIR after CU8 input
+    yields C64 samples, which the next stage must consume as C64 (advisor finding)."""
+    from sdrgpu import _lib
+    import scipy.signal as ss
+    f = sdr.filter
+    rate = 1.8e6
+    iq = _iq(30000, 2)
+    x = oracle.u8_to_c64(iq)
+    taps = ss.firwin(63, 0.3).astype(np.float32)
+    taps2 = ss.firwin(31, 0.4).astype(np.float32)
+    d = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
+                    f.BiquadD.LowPass(20000.0, 0.7))
+    src = lambda: sdr.signal.from_array(rate, iq, block=4096, sample_kind=_lib.CU8)
+    r = src().filter(taps).filter(d).collect()
+    y1 = oracle.Fir(taps, 1, sample_kind=1).process(x)
+    p = oracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
+    ro, rl = oracle.pll_batch(p, sdr.signal.from_array(rate, x).filter(taps).collect())
+    assert_parity(sdr.signal.from_array(rate, x).filter(taps).collect(), y1)
+    assert np.array_equal(r["value"], ro[0]) and np.array_equal(r["locked"], rl[0].astype(bool))
+    chain = src().filter(taps).filter(taps2).collect()
+    assert chain.dtype == np.complex64
+    assert_parity(chain, oracle.Fir(taps2, 1, sample_kind=1).process(y1))
+
+
+@pytest.mark.gpu
+def test_cu8_window_decimate_map_fft(sdr, oracle):
+    """examples/live.rs:29-39: rtl.listen().window(..).decimate(fps).map(fft) -- the raw bytes
+    go to the GPU STFT (u8 frame load) and equal the oracle STFT of the converted samples."""
+    from sdrgpu import _lib
+    iq = _iq(6000, 3)
+    n, hop, rate = 1000, 400, 1e6
+    y = (sdr.signal.from_array(rate, iq, block=777, sample_kind=_lib.CU8).window(n / rate)
+         .decimate(rate / hop).map(sdr.signal.fft).collect())
+    ref = oracle.stft(oracle.u8_to_c64(iq), n, hop)
+    assert y.shape == ref.shape
+    assert_parity(y, ref)

@@ -68,6 +68,75 @@ struct StreamSlot {
     }
 };
 
+// Asynchronous host streaming (the Block adapter's producer/consumer split,
+// src/signal/adapters/block.rs:105-207, with the GPU as the consumer): a block's H2D and
+// kernel go on the handle's stream, its download on a second stream, so block i's D2H
+// overlaps block i+1's H2D (PCIe is full duplex).  Two output slots of device staging, each
+// guarded by an event: a slot is rewritten only after its previous download finished.
+struct AsyncD2H {
+    static constexpr int kSlots = 2, kArrays = 2;
+    hipStream_t d2h = nullptr;
+    hipEvent_t ev_k[kSlots] = {}, ev_o[kSlots] = {};
+    bool live[kSlots] = {};
+    DevBuf out[kSlots][kArrays];
+    int next = 0;
+
+    int init() {
+        if (d2h) return SDRGPU_OK;
+        if (hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) return SDRGPU_ERR_DEVICE;
+        for (int i = 0; i < kSlots; ++i)
+            if (hipEventCreateWithFlags(&ev_k[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ev_o[i], hipEventDisableTiming) != hipSuccess)
+                return SDRGPU_ERR_DEVICE;
+        return SDRGPU_OK;
+    }
+    // next slot with `bytes[a]` of device staging per output array; `s` (the compute stream)
+    // waits for the slot's previous download before anything later on it writes the slot
+    int acquire(hipStream_t s, const size_t* bytes, int narrays, int* slot) {
+        int st = init();
+        if (st) return st;
+        const int k = next;
+        next = (next + 1) % kSlots;
+        for (int a = 0; a < narrays; ++a)
+            if (out[k][a].cap < bytes[a]) {
+                if (hipStreamSynchronize(d2h) != hipSuccess) return SDRGPU_ERR_DEVICE;
+                live[k] = false;
+                if ((st = out[k][a].ensure(bytes[a]))) return st;
+            }
+        if (live[k] && hipStreamWaitEvent(s, ev_o[k], 0) != hipSuccess) return SDRGPU_ERR_DEVICE;
+        *slot = k;
+        return SDRGPU_OK;
+    }
+    // after the producing kernel on `s`: the download stream waits for it
+    int begin_download(hipStream_t s, int slot) {
+        if (hipEventRecord(ev_k[slot], s) != hipSuccess ||
+            hipStreamWaitEvent(d2h, ev_k[slot], 0) != hipSuccess)
+            return SDRGPU_ERR_DEVICE;
+        return SDRGPU_OK;
+    }
+    int end_download(int slot) {
+        if (hipEventRecord(ev_o[slot], d2h) != hipSuccess) return SDRGPU_ERR_DEVICE;
+        live[slot] = true;
+        return SDRGPU_OK;
+    }
+    int sync() {
+        if (d2h && hipStreamSynchronize(d2h) != hipSuccess) return SDRGPU_ERR_DEVICE;
+        return SDRGPU_OK;
+    }
+    void release() {
+        if (d2h) (void)hipStreamSynchronize(d2h);
+        for (int i = 0; i < kSlots; ++i) {
+            for (auto& b : out[i]) b.release();
+            if (ev_k[i]) (void)hipEventDestroy(ev_k[i]);
+            if (ev_o[i]) (void)hipEventDestroy(ev_o[i]);
+            ev_k[i] = ev_o[i] = nullptr;
+            live[i] = false;
+        }
+        if (d2h) (void)hipStreamDestroy(d2h);
+        d2h = nullptr;
+    }
+};
+
 // BiquadD::design -> Biquad::new coefficients b0 b1 b2 na1 na2 (abi_pll.cpp)
 int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident);
 

@@ -12,9 +12,12 @@ using namespace sdrgpu::detail;
 struct sdrgpu_fft {
     int device = 0;
     int n = 0;
+    int out_db = 0;  // SDRGPU_FFT_OUT_DB: f32 dB magnitudes instead of C64 values
     void* plan = nullptr;
     StreamSlot stream;
     DevBuf stage_in, stage_out, scratch;
+    AsyncD2H async;
+    size_t out_elem() const { return out_db ? sizeof(float) : sizeof(float2); }
 
     int ensure_scratch() {
         const size_t b = fft_scratch_bytes(plan);
@@ -26,6 +29,7 @@ struct sdrgpu_fft {
         stage_in.release();
         stage_out.release();
         scratch.release();
+        async.release();
         if (plan) fft_plan_destroy(plan);
         plan = nullptr;
         stream.destroy();
@@ -33,6 +37,7 @@ struct sdrgpu_fft {
     int run(const FftFrames& fr, float2* out, int store_mode) {
         int st = ensure_scratch();
         if (st) return st;
+        if (out_db) store_mode += 3;  // collated / rfft as dB magnitudes
         return fft_launch(plan, fr, out, store_mode, static_cast<float2*>(scratch.ptr),
                           fft_scratch_frames(plan), stream.cur);
     }
@@ -54,6 +59,7 @@ struct sdrgpu_stft {
     sdrgpu_fft fft;
     long hop = 1;
     long H = 0;  // n - 1 history samples
+    int in_kind = SDRGPU_C64;  // or SDRGPU_CU8 (rtl_tcp bytes, converted in the frame load)
     float2* d_hist[2] = {nullptr, nullptr};
     int cur = 0;
     unsigned long long seen = 0;
@@ -116,11 +122,12 @@ int sdrgpu_fft_exec(sdrgpu_fft* h, const void* in, void* out, size_t count) {
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
     const size_t bytes = count * (size_t)h->n * sizeof(float2);
+    const size_t obytes = count * (size_t)h->n * h->out_elem();
     int st;
-    if ((st = h->stage_in.ensure(bytes)) || (st = h->stage_out.ensure(bytes))) return st;
+    if ((st = h->stage_in.ensure(bytes)) || (st = h->stage_out.ensure(obytes))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(h->stage_in.ptr, in, bytes, hipMemcpyHostToDevice, h->stream.cur));
     if ((st = sdrgpu_fft_exec_dev(h, h->stage_in.ptr, h->stage_out.ptr, count))) return st;
-    SDRGPU_HIP_TRY(hipMemcpyAsync(out, h->stage_out.ptr, bytes, hipMemcpyDeviceToHost, h->stream.cur));
+    SDRGPU_HIP_TRY(hipMemcpyAsync(out, h->stage_out.ptr, obytes, hipMemcpyDeviceToHost, h->stream.cur));
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
     return SDRGPU_OK;
 }
@@ -132,7 +139,7 @@ int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count) {
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
     const size_t in_bytes = count * (size_t)h->n * sizeof(float);
-    const size_t out_bytes = count * (size_t)(h->n - h->n / 2) * sizeof(float2);
+    const size_t out_bytes = count * (size_t)(h->n - h->n / 2) * h->out_elem();
     int st;
     if ((st = h->stage_in.ensure(in_bytes)) || (st = h->stage_out.ensure(out_bytes))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(h->stage_in.ptr, in, in_bytes, hipMemcpyHostToDevice, h->stream.cur));
@@ -146,11 +153,17 @@ int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_fft_set_output(sdrgpu_fft* h, int mode) {
+    if (!h || (mode != SDRGPU_FFT_OUT_COMPLEX && mode != SDRGPU_FFT_OUT_DB)) return SDRGPU_ERR_INVALID;
+    h->out_db = mode == SDRGPU_FFT_OUT_DB;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_fft_sync(sdrgpu_fft* h) {
     if (!h) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
-    return SDRGPU_OK;
+    return h->async.sync();
 }
 
 void sdrgpu_fft_destroy(sdrgpu_fft* h) {
@@ -224,8 +237,10 @@ int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void*
     DeviceGuard g(h->fft.device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
     FftFrames fr{};
-    fr.mode = 1;
+    const bool u8 = h->in_kind == SDRGPU_CU8;
+    fr.mode = u8 ? 3 : 1;
     fr.in = static_cast<const float2*>(d_in);
+    fr.in_u8 = static_cast<const unsigned short*>(d_in);
     fr.n_in = (long)n_in;
     fr.hist = h->d_hist[h->cur];
     fr.H = h->H;
@@ -234,8 +249,10 @@ int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void*
     fr.nframes = (long)nf;
     int st = h->fft.run(fr, static_cast<float2*>(d_out), 0);
     if (st) return st;
-    st = stft_carry_launch(fr.in, fr.n_in, h->d_hist[h->cur], h->d_hist[h->cur ^ 1], h->H,
-                           h->fft.stream.cur);
+    st = u8 ? stft_carry_u8_launch(fr.in_u8, fr.n_in, h->d_hist[h->cur], h->d_hist[h->cur ^ 1],
+                                   h->H, h->fft.stream.cur)
+            : stft_carry_launch(fr.in, fr.n_in, h->d_hist[h->cur], h->d_hist[h->cur ^ 1], h->H,
+                                h->fft.stream.cur);
     if (st) return st;
     h->cur ^= 1;
     h->seen += n_in;
@@ -252,7 +269,7 @@ int sdrgpu_stft_process(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
     if (!in || (nf && !out)) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->fft.device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
-    const size_t ib = n_in * sizeof(float2), ob = nf * (size_t)h->fft.n * sizeof(float2);
+    const size_t ib = n_in * kind_bytes(h->in_kind), ob = nf * (size_t)h->fft.n * h->fft.out_elem();
     int st;
     if ((st = h->fft.stage_in.ensure(ib)) || (st = h->fft.stage_out.ensure(ob ? ob : 8))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(h->fft.stage_in.ptr, in, ib, hipMemcpyHostToDevice, h->fft.stream.cur));
@@ -265,9 +282,55 @@ int sdrgpu_stft_process(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
     return SDRGPU_OK;
 }
 
+int sdrgpu_stft_process_async(sdrgpu_stft* h, const void* in, size_t n_in, void* out,
+                              size_t out_cap_frames, size_t* n_frames) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    const size_t nf = h->frames_for(n_in);
+    if (n_frames) *n_frames = nf;
+    if (nf > out_cap_frames) return SDRGPU_ERR_OUTPUT_CAP;
+    if (n_in == 0) return SDRGPU_OK;
+    if (!in || (nf && !out)) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->fft.device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    sdrgpu_fft& f = h->fft;
+    const size_t ib = n_in * kind_bytes(h->in_kind), ob = nf * (size_t)f.n * f.out_elem();
+    int st, slot = 0;
+    if (f.stage_in.cap < ib) {  // growing frees a buffer an earlier block may still read
+        SDRGPU_HIP_TRY(hipStreamSynchronize(f.stream.cur));
+        if ((st = f.stage_in.ensure(ib))) return st;
+    }
+    const size_t obytes[1] = {ob ? ob : 8};
+    if ((st = f.async.acquire(f.stream.cur, obytes, 1, &slot))) return st;
+    SDRGPU_HIP_TRY(hipMemcpyAsync(f.stage_in.ptr, in, ib, hipMemcpyHostToDevice, f.stream.cur));
+    size_t got = 0;
+    if ((st = sdrgpu_stft_process_dev(h, f.stage_in.ptr, n_in, f.async.out[slot][0].ptr, nf, &got)))
+        return st;
+    if (ob) {
+        if ((st = f.async.begin_download(f.stream.cur, slot))) return st;
+        SDRGPU_HIP_TRY(hipMemcpyAsync(out, f.async.out[slot][0].ptr, ob, hipMemcpyDeviceToHost,
+                                      f.async.d2h));
+        if ((st = f.async.end_download(slot))) return st;
+    }
+    return SDRGPU_OK;
+}
+
+int sdrgpu_stft_set_input_kind(sdrgpu_stft* h, int sample_kind) {
+    if (!h || (sample_kind != SDRGPU_C64 && sample_kind != SDRGPU_CU8)) return SDRGPU_ERR_INVALID;
+    h->in_kind = sample_kind;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_stft_set_output(sdrgpu_stft* h, int mode) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    return sdrgpu_fft_set_output(&h->fft, mode);
+}
+
 int sdrgpu_stft_sync(sdrgpu_stft* h) {
     if (!h) return SDRGPU_ERR_INVALID;
-    return sdrgpu_fft_sync(&h->fft);
+    int st = sdrgpu_fft_sync(&h->fft);
+    if (st) return st;
+    DeviceGuard g(h->fft.device);
+    return h->fft.async.sync();
 }
 
 int sdrgpu_stft_reset(sdrgpu_stft* h) {

@@ -68,11 +68,13 @@ struct sdrgpu_pll {
     PllChannelState* d_state = nullptr;
     StreamSlot stream;
     DevBuf stage_in, stage_out, stage_lock;
+    AsyncD2H async;
 
     void free_all() {
         DeviceGuard g(device);
         if (d_state) (void)hipFree(d_state);
         d_state = nullptr;
+        async.release();
         stage_in.release();
         stage_out.release();
         stage_lock.release();
@@ -192,6 +194,35 @@ int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, fl
     return SDRGPU_OK;
 }
 
+int sdrgpu_pll_process_async(sdrgpu_pll* h, const void* in, size_t n, float* out,
+                             uint8_t* locked) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    if (n == 0) return SDRGPU_OK;
+    if (!in || !out || !locked) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    const size_t nch = (size_t)h->dp.nch;
+    const size_t sb = h->dp.in_u8 ? 2 : sizeof(float2);
+    int st, slot = 0;
+    if (h->stage_in.cap < nch * n * sb) {  // growing frees a buffer an earlier block may read
+        SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+        if ((st = h->stage_in.ensure(nch * n * sb))) return st;
+    }
+    const size_t ob[2] = {nch * n * sizeof(float), nch * n};
+    if ((st = h->async.acquire(h->stream.cur, ob, 2, &slot))) return st;
+    SDRGPU_HIP_TRY(hipMemcpyAsync(h->stage_in.ptr, in, nch * n * sb, hipMemcpyHostToDevice,
+                                  h->stream.cur));
+    float* d_out = static_cast<float*>(h->async.out[slot][0].ptr);
+    uint8_t* d_lock = static_cast<uint8_t*>(h->async.out[slot][1].ptr);
+    if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n, d_out, d_lock, (long)n,
+                         h->d_state, h->stream.cur)))
+        return st;
+    if ((st = h->async.begin_download(h->stream.cur, slot))) return st;
+    SDRGPU_HIP_TRY(hipMemcpyAsync(out, d_out, ob[0], hipMemcpyDeviceToHost, h->async.d2h));
+    SDRGPU_HIP_TRY(hipMemcpyAsync(locked, d_lock, ob[1], hipMemcpyDeviceToHost, h->async.d2h));
+    return h->async.end_download(slot);
+}
+
 int sdrgpu_pll_state(sdrgpu_pll* h, size_t ch, float* nphase, float* value_re_im) {
     if (!h || (long)ch >= h->dp.nch) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
@@ -210,7 +241,7 @@ int sdrgpu_pll_sync(sdrgpu_pll* h) {
     if (!h) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
-    return SDRGPU_OK;
+    return h->async.sync();
 }
 
 int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {

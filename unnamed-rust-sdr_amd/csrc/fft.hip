@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
     }
     __syncthreads();
     tile_fft<M, false>(lds, a.tw);
-    if (a.store_mode == 0) {
+    if (a.store_mode == 0 || a.store_mode == 3) {
         // collated store, output-ordered (coalesced): out[f][i] = X[(i + M/2) % M] * norm
         const int half = M / 2;
 #pragma unroll 4
@@ -129,7 +129,8 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
                 int k = o + half;
                 if (k >= M) k -= M;
                 float2 x = lds[fpad(f * M + k)];
-                a.out[(f0 + f) * M + o] = make_float2(x.x * a.norm, x.y * a.norm);
+                if (a.store_mode == 0) a.out[(f0 + f) * M + o] = make_float2(x.x * a.norm, x.y * a.norm);
+                else reinterpret_cast<float*>(a.out)[(f0 + f) * M + o] = db_of(x, a.norm);
             }
         }
     } else {
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(16 * CB) void fft64k_pass_a(F64Args a) {
     const FrameSrc& s = a.src;
     long g0 = 0;
     bool fast = s.mode == 0;
-    if (s.mode == 1) {
+    if (s.mode == 1) {  // (u8 streams, mode 3, take the generic frame_sample path)
         g0 = s.first_end + f * s.hop - M;
         fast = g0 >= 0 && g0 + M <= s.n_in;
     }
@@ -462,6 +463,7 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
     src.mode = fr.mode;
     src.in = fr.in;
     src.in_real = fr.in_real;
+    src.in_u8 = fr.in_u8;
     src.n_in = fr.n_in;
     src.hist = fr.hist;
     src.H = fr.H;
@@ -498,7 +500,6 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         return SDRGPU_OK;
     }
     if (!scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
-    const long ostride = store_mode == 1 ? p->M - p->M / 2 : p->M;  // output samples per frame
     static const bool use64 = [] {
         const char* e = getenv("SDRGPU_FFT64K");
         return !e || atoi(e) != 0;
@@ -541,10 +542,11 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
             hipStream_t st = odd ? p->aux : s;
             a.scratch = scratch + (odd ? batch * (long)p->M : 0L);
             a.src = src;
-            if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
+            if (frame_src_is_stream(src.mode)) a.src.first_end = src.first_end + f0 * src.hop;
             else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
+            else a.src.in_real = src.in_real + f0 * (long)p->M;
             a.nframes = nf;
-            a.out = out + f0 * ostride;
+            a.out = store_advance(out, f0, p->M, store_mode);
             const dim3 g((unsigned)(nf * (256 / cb))), b(16 * cb);
             if (cb == 64 && nt) {
                 hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, st, a);
@@ -584,10 +586,11 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
     for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
         const long nf = std::min((long)scratch_frames, fr.nframes - f0);
         a.src = src;
-        if (src.mode == 1) a.src.first_end = src.first_end + f0 * src.hop;
+        if (frame_src_is_stream(src.mode)) a.src.first_end = src.first_end + f0 * src.hop;
         else if (src.mode == 0) a.src.in = src.in + f0 * (long)p->M;
+        else a.src.in_real = src.in_real + f0 * (long)p->M;
         a.nframes = nf;
-        a.out = out + f0 * ostride;
+        a.out = store_advance(out, f0, p->M, store_mode);
         const long ga = nf * (a.M1 / (kTile / a.M2));
         const long gb = nf * (a.M2 / (kTile / a.M1));
         const dim3 bA((unsigned)ga), bB((unsigned)gb), b(kFftBlock);
@@ -619,6 +622,24 @@ __global__ void stft_carry_kernel(const float2* in, long n_in, const float2* his
         const long g = n_in - H + j;
         hist_next[j] = g >= 0 ? in[g] : hist[g + H];
     }
+}
+
+__global__ void stft_carry_u8_kernel(const unsigned short* in, long n_in, const float2* hist,
+                                     float2* hist_next, long H) {
+    for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < H; j += (long)gridDim.x * blockDim.x) {
+        const long g = n_in - H + j;
+        hist_next[j] = g >= 0 ? u8_sample(in[g]) : hist[g + H];
+    }
+}
+
+int stft_carry_u8_launch(const unsigned short* in, long n_in, const float2* hist,
+                         float2* hist_next, long H, hipStream_t s) {
+    if (H <= 0) return SDRGPU_OK;
+    const long nb = std::min<long>((H + 255) / 256, 1024);
+    hipLaunchKernelGGL(stft_carry_u8_kernel, dim3((unsigned)nb), dim3(256), 0, s, in, n_in, hist,
+                       hist_next, H);
+    SDRGPU_LAUNCH_CHECK();
+    return SDRGPU_OK;
 }
 
 int stft_carry_launch(const float2* in, long n_in, const float2* hist, float2* hist_next, long H,

@@ -12,9 +12,12 @@ struct FrameSrc {
     // mode 1: STFT frames from a stream: frame f covers stream [f0 + (f+1)hop - M, +M), stream
     //         index g < 0 -> hist[g + H] (H = history length) if g >= -H, else 0; g >= n_in -> 0
     // mode 2: contiguous REAL frames (float, imag = 0) -- rfft
+    // mode 3: as mode 1 from an rtl_tcp u8 I/Q stream (RtlTcpSignal::next, src/rtltcp.rs:156-164,
+    //         converted in the load: (v - 128) / 128); the history stays C64
     int mode;
     const float2* in;
     const float* in_real;
+    const unsigned short* in_u8;
     long n_in;
     const float2* hist;
     long H;
@@ -22,31 +25,60 @@ struct FrameSrc {
     long hop;
 };
 
+__host__ __device__ inline bool frame_src_is_stream(int mode) { return mode == 1 || mode == 3; }
+
+__device__ __forceinline__ float2 u8_sample(unsigned short w) {
+    return make_float2(((float)(w & 0xffu) - 128.0f) / 128.0f, ((float)(w >> 8) - 128.0f) / 128.0f);
+}
+
 __device__ __forceinline__ float2 frame_sample(const FrameSrc& s, long M, long f, long n) {
     if (s.mode == 0) return s.in[f * M + n];
     if (s.mode == 2) return make_float2(s.in_real[f * M + n], 0.f);
     const long g = s.first_end + f * s.hop - M + n;
-    if (g >= 0) return g < s.n_in ? s.in[g] : make_float2(0.f, 0.f);
+    if (g >= 0) {
+        if (g >= s.n_in) return make_float2(0.f, 0.f);
+        return s.mode == 3 ? u8_sample(s.in_u8[g]) : s.in[g];
+    }
     if (g >= -s.H) return s.hist[g + s.H];
     return make_float2(0.f, 0.f);
 }
 
-// bin k of frame f by store mode: 0 collated fft (out[(k + M/2) mod M] * norm, fft.rs:14-26),
-// 1 rfft (collated [M/2, M) = X[0, M - M/2) * norm, fft.rs:35), 2 natural order, unscaled
-// (internal: the power-of-two transforms inside Bluestein)
+// Store modes (bin k of frame f):
+//   0 collated fft: out[(k + M/2) mod M] = X[k] * norm (fft.rs:14-26)
+//   1 rfft: collated [M/2, M) = X[0, M - M/2) * norm (fft.rs:35)
+//   2 natural order, unscaled (internal: the power-of-two transforms inside Bluestein)
+//   3 / 4 as 0 / 1 but the f32 magnitude in dB, 20 log10(|X * norm|) -- the spectrum plots'
+//     conversion (src/plot/complexseries.rs:90-92: y.norm(), then 20 * log10)
+__host__ __device__ inline long store_stride(int mode, long M) {
+    return (mode == 1 || mode == 4) ? M - M / 2 : M;
+}
+__host__ __device__ inline long store_elem_bytes(int mode) { return mode >= 3 ? 4 : 8; }
+// output pointer advanced by `frames` frames
+__host__ __device__ inline float2* store_advance(float2* out, long frames, long M, int mode) {
+    return reinterpret_cast<float2*>(reinterpret_cast<char*>(out) +
+                                     frames * store_stride(mode, M) * store_elem_bytes(mode));
+}
+
+__device__ __forceinline__ float db_of(float2 x, float norm) {
+    return 20.0f * log10f(hypotf(x.x * norm, x.y * norm));
+}
+
 __device__ __forceinline__ void store_bin(float2* __restrict__ out, long f, long M, long k,
                                           float2 x, int mode, float norm) {
-    if (mode == 0) {
+    if (mode == 0 || mode == 3) {
         long o = k + M / 2;
         if (o >= M) o -= M;
-        out[f * M + o] = make_float2(x.x * norm, x.y * norm);
-    } else if (mode == 1) {
+        if (mode == 0) out[f * M + o] = make_float2(x.x * norm, x.y * norm);
+        else reinterpret_cast<float*>(out)[f * M + o] = db_of(x, norm);
+    } else if (mode == 1 || mode == 4) {
         const long keep = M - M / 2;
-        if (k < keep) out[f * keep + k] = make_float2(x.x * norm, x.y * norm);
+        if (k < keep) {
+            if (mode == 1) out[f * keep + k] = make_float2(x.x * norm, x.y * norm);
+            else reinterpret_cast<float*>(out)[f * keep + k] = db_of(x, norm);
+        }
     } else {
         out[f * M + k] = x;
     }
 }
-
 
 }  // namespace sdrgpu

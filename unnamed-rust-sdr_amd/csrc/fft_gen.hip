@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
     }
     __syncthreads();
     const float2* X = gen_engine(b0, b1, N, B, a.rl, a.tw);
-    if (a.store_mode == 0) {
+    if (a.store_mode == 0 || a.store_mode == 3) {
         // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o
         const int sh = N - N / 2;
         for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
@@ -218,7 +218,8 @@ __global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
             int k = o + sh;
             if (k >= N) k -= N;
             const float2 x = X[f * N + k];
-            a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
+            if (a.store_mode == 0) a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
+            else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);
         }
     } else {
         for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
@@ -500,15 +501,15 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
     src.mode = fr.mode;
     src.in = fr.in;
     src.in_real = fr.in_real;
+    src.in_u8 = fr.in_u8;
     src.n_in = fr.n_in;
     src.hist = fr.hist;
     src.H = fr.H;
     src.first_end = fr.first_end;
     src.hop = fr.hop;
     const long N = p->N;
-    const long ostride = store_mode == 1 ? N - N / 2 : N;
     auto advance = [&](FrameSrc& a, long f0) {
-        if (a.mode == 1) a.first_end += f0 * a.hop;
+        if (frame_src_is_stream(a.mode)) a.first_end += f0 * a.hop;
         else if (a.mode == 0) a.in += f0 * N;
         else a.in_real += f0 * N;
     };
@@ -550,7 +551,7 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
             a.src = src;
             advance(a.src, f0);
             a.nframes = nf;
-            a.out = out + f0 * ostride;
+            a.out = store_advance(out, f0, N, store_mode);
             hipLaunchKernelGGL(gen4_pass_a, dim3((unsigned)(nf * ta)), dim3(kGenBlock),
                                2 * (size_t)std::min(CA, p->N1) * p->N2 * sizeof(float2), s, a);
             SDRGPU_LAUNCH_CHECK();
@@ -577,7 +578,7 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         a.src = src;
         advance(a.src, f0);
         a.nframes = nf;
-        a.out = out + f0 * ostride;
+        a.out = store_advance(out, f0, N, store_mode);
         const unsigned g = (unsigned)std::min<long>(4096, (nf * M + 255) / 256);
         hipLaunchKernelGGL(blu_pre, dim3(g), dim3(256), 0, s, a);
         SDRGPU_LAUNCH_CHECK();

@@ -30,6 +30,9 @@ FIR_DIRECT = 1
 FIR_OVERLAP_SAVE = 2
 FIR_MATRIX = 3
 
+FFT_OUT_COMPLEX = 0
+FFT_OUT_DB = 1
+
 PLL_OUT_FILTER = 0
 PLL_OUT_STEREO_DIFF = 1
 
@@ -123,6 +126,7 @@ SIGNATURES = [
     ("sdrgpu_fft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_fft_exec_dev", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_rfft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
+    ("sdrgpu_fft_set_output", c_int, [_H, c_int]),
     ("sdrgpu_fft_sync", c_int, [_H]),
     ("sdrgpu_fft_destroy", None, [_H]),
     ("sdrgpu_fft_freqs", c_int, [c_size_t, c_float, c_void_p]),
@@ -133,6 +137,9 @@ SIGNATURES = [
     ("sdrgpu_stft_output_len", c_int, [_H, c_size_t, _PS]),
     ("sdrgpu_stft_process", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_stft_process_dev", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
+    ("sdrgpu_stft_process_async", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
+    ("sdrgpu_stft_set_input_kind", c_int, [_H, c_int]),
+    ("sdrgpu_stft_set_output", c_int, [_H, c_int]),
     ("sdrgpu_stft_sync", c_int, [_H]),
     ("sdrgpu_stft_reset", c_int, [_H]),
     ("sdrgpu_stft_destroy", None, [_H]),
@@ -146,6 +153,7 @@ SIGNATURES = [
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_pll_process_dev", c_int,
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p, c_size_t]),
+    ("sdrgpu_pll_process_async", c_int, [_H, c_void_p, c_size_t, c_void_p, c_void_p]),
     ("sdrgpu_pll_state", c_int, [_H, c_size_t, POINTER(c_float), POINTER(c_float)]),
     ("sdrgpu_pll_sync", c_int, [_H]),
     ("sdrgpu_pll_reset", c_int, [_H]),

@@ -26,14 +26,26 @@ def freqs(n: int, rate: float) -> np.ndarray:
     return out
 
 
-class FftPlan:
-    """A planned N-point forward FFT with fft.rs collation (plan once, unlike fft.rs:10-11)."""
+def _out_mode(output: str) -> int:
+    if output not in ("complex", "db"):
+        raise _lib.SdrGpuError(_lib.ERR_INVALID, "output must be 'complex' or 'db'")
+    return _lib.FFT_OUT_DB if output == "db" else _lib.FFT_OUT_COMPLEX
 
-    def __init__(self, n: int, device: int = 0):
+
+class FftPlan:
+    """A planned N-point forward FFT with fft.rs collation (plan once, unlike fft.rs:10-11).
+
+    output='db' returns f32 20*log10(|value|) per bin instead of the complex value -- the
+    spectrum plots' conversion (src/plot/complexseries.rs:90-92) fused into the store."""
+
+    def __init__(self, n: int, device: int = 0, output: str = "complex"):
         self.n = int(n)
         self.device = device
+        self.output = output
         self._h = ctypes.c_void_p()
         check(lib().sdrgpu_fft_plan(device, self.n, ctypes.byref(self._h)), "sdrgpu_fft_plan")
+        check(lib().sdrgpu_fft_set_output(self._h, _out_mode(output)), "sdrgpu_fft_set_output")
+        self._odt = np.float32 if output == "db" else np.complex64
 
     def close(self):
         if self._h:
@@ -56,7 +68,7 @@ class FftPlan:
         x = np.ascontiguousarray(x, np.complex64)
         squeeze = x.ndim == 1
         x2 = x.reshape(-1, self.n)
-        out = np.empty_like(x2)
+        out = np.empty(x2.shape, self._odt)
         check(lib().sdrgpu_fft_exec(self._h, x2.ctypes.data, out.ctypes.data, x2.shape[0]),
               "sdrgpu_fft_exec")
         return out[0] if squeeze else out
@@ -67,7 +79,7 @@ class FftPlan:
         x = np.ascontiguousarray(x, np.float32)
         squeeze = x.ndim == 1
         x2 = x.reshape(-1, self.n)
-        out = np.empty((x2.shape[0], self.n - self.n // 2), np.complex64)
+        out = np.empty((x2.shape[0], self.n - self.n // 2), self._odt)
         check(lib().sdrgpu_rfft_exec(self._h, x2.ctypes.data, out.ctypes.data, x2.shape[0]),
               "sdrgpu_rfft_exec")
         return out[0] if squeeze else out
@@ -94,13 +106,29 @@ def rfft(x, rate: float, device: int = 0):
 
 
 class Stft:
-    """Streaming Window(n) + Decimate(hop) + fft (adapters/mod.rs:270-303, 13-41)."""
+    """Streaming Window(n) + Decimate(hop) + fft (adapters/mod.rs:270-303, 13-41).
 
-    def __init__(self, n: int, hop: int, device: int = 0):
+    input_kind=CU8 takes raw rtl_tcp I/Q bytes (examples/live.rs windows rtl.listen()
+    directly); output='db' yields f32 dB magnitudes (src/plot/complexseries.rs:90-92)."""
+
+    def __init__(self, n: int, hop: int, device: int = 0, input_kind: int = _lib.C64,
+                 output: str = "complex"):
         self.n, self.hop, self.device = int(n), int(hop), device
+        self.input_kind, self.output = input_kind, output
+        self._odt = np.float32 if output == "db" else np.complex64
         self._h = ctypes.c_void_p()
         check(lib().sdrgpu_stft_create(device, self.n, self.hop, ctypes.byref(self._h)),
               "sdrgpu_stft_create")
+        check(lib().sdrgpu_stft_set_input_kind(self._h, input_kind), "sdrgpu_stft_set_input_kind")
+        check(lib().sdrgpu_stft_set_output(self._h, _out_mode(output)), "sdrgpu_stft_set_output")
+
+    def _as_in(self, x):
+        if self.input_kind == _lib.CU8:
+            return np.ascontiguousarray(x, np.uint8).reshape(-1)
+        return np.ascontiguousarray(x, np.complex64)
+
+    def _nsamp(self, x):
+        return x.size // 2 if self.input_kind == _lib.CU8 else x.size
 
     def close(self):
         if self._h:
@@ -124,13 +152,22 @@ class Stft:
         return n.value
 
     def process(self, x) -> np.ndarray:
-        x = np.ascontiguousarray(x, np.complex64)
-        nf = self.output_len(x.size)
-        out = np.empty((max(nf, 1), self.n), np.complex64)
+        x = self._as_in(x)
+        ns = self._nsamp(x)
+        nf = self.output_len(ns)
+        out = np.empty((max(nf, 1), self.n), self._odt)
         got = ctypes.c_size_t()
-        check(lib().sdrgpu_stft_process(self._h, x.ctypes.data, x.size, out.ctypes.data,
+        check(lib().sdrgpu_stft_process(self._h, x.ctypes.data, ns, out.ctypes.data,
                                         nf, ctypes.byref(got)), "sdrgpu_stft_process")
         return out[:got.value]
+
+    def process_async(self, in_ptr: int, n_in: int, out_ptr: int, cap_frames: int) -> int:
+        """Pinned host blocks (device.PinnedBuffer), enqueued without waiting; returns the
+        frame count.  Read the output after sync()."""
+        got = ctypes.c_size_t()
+        check(lib().sdrgpu_stft_process_async(self._h, in_ptr, n_in, out_ptr, cap_frames,
+                                              ctypes.byref(got)), "sdrgpu_stft_process_async")
+        return got.value
 
     def process_dev(self, d_in: int, n_in: int, d_out: int, cap_frames: int) -> int:
         got = ctypes.c_size_t()

@@ -463,6 +463,11 @@ class Pll:
     def reset(self):
         check(lib().sdrgpu_pll_reset(self._h), "sdrgpu_pll_reset")
 
+    def set_input_kind(self, kind: int):
+        """_lib.C64 (default) or _lib.CU8 (raw rtl_tcp I/Q bytes) for process_dev /
+        process_async (process / process_u8 set it themselves)."""
+        check(lib().sdrgpu_pll_set_input_kind(self._h, kind), "sdrgpu_pll_set_input_kind")
+
     def set_output_mode(self, mode: int):
         """_lib.PLL_OUT_FILTER (Pll::apply's output) or _lib.PLL_OUT_STEREO_DIFF."""
         check(lib().sdrgpu_pll_set_output_mode(self._h, mode), "sdrgpu_pll_set_output_mode")
@@ -525,6 +530,12 @@ class Pll:
         """Filter::apply (pll.rs:70-85): Some(output) or None."""
         o, l = self.process(np.asarray([value], dtype=np.complex64))
         return float(o[0]) if l[0] else None
+
+    def process_async(self, in_ptr: int, n: int, out_ptr: int, locked_ptr: int):
+        """Pinned host blocks of nch x n samples (dense), enqueued without waiting; read the
+        outputs after sync()."""
+        check(lib().sdrgpu_pll_process_async(self._h, in_ptr, n, out_ptr, locked_ptr),
+              "sdrgpu_pll_process_async")
 
     def process_dev(self, d_in, ld_in, n, d_out, d_locked, ld_out):
         check(lib().sdrgpu_pll_process_dev(self._h, d_in, ld_in, n, d_out, d_locked, ld_out),

@@ -19,8 +19,8 @@ reference names and argument meaning:
                      through resample.SampleRate (GPU ZOH / linear); rate() = the new rate
   map(f), take(duration), skip(duration), iter(), collect()
 
-Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), impulse
-(sources.rs:223-257).
+Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), freq_sweep
+(sources.rs:116-194), impulse (sources.rs:223-257).
 """
 from __future__ import annotations
 
@@ -34,6 +34,27 @@ from . import fft as _fft
 from . import resample as _resample
 
 DEFAULT_BLOCK = 1 << 16
+
+
+# rtl_tcp blocks (sample_kind CU8) are raw interleaved I/Q bytes, 2 per sample: the sample-
+# counting adapters below index them in sample units (byte pairs), never single bytes
+def _nsamples(b, kind) -> int:
+    return b.size // 2 if kind == _lib.CU8 else len(b)
+
+
+def _pairs(b, kind):
+    return np.asarray(b).reshape(-1, 2) if kind == _lib.CU8 else b
+
+
+def _unpairs(b, kind):
+    return b.reshape(-1) if kind == _lib.CU8 else b
+
+
+def _cu8_values(b) -> np.ndarray:
+    """RtlTcpSignal::next (src/rtltcp.rs:156-164): (v - 128) / 128, for host-side adapters
+    that hand samples to arbitrary Python code (the GPU stages read the bytes directly)."""
+    v = (np.asarray(b, np.float32).reshape(-1, 2) - np.float32(128.0)) / np.float32(128.0)
+    return (v[:, 0] + 1j * v[:, 1]).astype(np.complex64)
 
 
 class Signal:
@@ -81,7 +102,9 @@ class Signal:
                 y = f.process(b)
                 if y.size:
                     yield y
-        return Signal(self._rate, gen, sk, _fir={"up": up, "fir": fir, "decim": decim})
+        # rtl_tcp bytes in, Complex<f32> out: downstream stages see C64 samples
+        out_kind = _lib.C64 if sk == _lib.CU8 else sk
+        return Signal(self._rate, gen, out_kind, _fir={"up": up, "fir": fir, "decim": decim})
 
     def _pll(self, design: "_filter.PllDesign") -> "Signal":
         up = self
@@ -106,14 +129,15 @@ class Signal:
         if getattr(self, "_window", None) is not None:
             return _WindowDecimate(self, self._window, wait)
         up = self
+        sk = self.sample_kind
 
         def gen():
             phase = 0  # samples consumed mod wait
             for b in up.blocks():
                 first = (wait - 1 - phase) % wait
-                yield b[first::wait]
-                phase = (phase + len(b)) % wait
-        return Signal(self._rate, gen, self.sample_kind)  # Decimate::rate quirk (:38-40)
+                yield _unpairs(_pairs(b, sk)[first::wait], sk)
+                phase = (phase + _nsamples(b, sk)) % wait
+        return Signal(self._rate, gen, sk)  # Decimate::rate quirk (:38-40)
 
     def resample(self, rate: float) -> "Signal":
         """Signal::resample (src/signal/mod.rs:78-84): SincBestQuality, which this build
@@ -188,29 +212,32 @@ class Signal:
     def take(self, duration: float) -> "Signal":
         n = int(round(self._rate * duration))
         up = self
+        sk = self.sample_kind
 
         def gen():
             left = n
             for b in up.blocks():
                 if left <= 0:
                     return
-                yield b[:left]
-                left -= len(b)
-        return Signal(self._rate, gen, self.sample_kind)
+                yield _unpairs(_pairs(b, sk)[:left], sk)
+                left -= _nsamples(b, sk)
+        return Signal(self._rate, gen, sk)
 
     def skip(self, duration: float) -> "Signal":
         n = int(round(self._rate * duration))
         up = self
+        sk = self.sample_kind
 
         def gen():
             left = n
             for b in up.blocks():
-                if left >= len(b):
-                    left -= len(b)
+                nb = _nsamples(b, sk)
+                if left >= nb:
+                    left -= nb
                     continue
-                yield b[left:]
+                yield _unpairs(_pairs(b, sk)[left:], sk)
                 left = 0
-        return Signal(self._rate, gen, self.sample_kind)
+        return Signal(self._rate, gen, sk)
 
 
 class _WindowDecimate(Signal):
@@ -224,6 +251,8 @@ class _WindowDecimate(Signal):
             buf = np.zeros(cap, np.complex64)
             phase = 0
             for b in up.blocks():
+                if up.sample_kind == _lib.CU8:
+                    b = _cu8_values(b)
                 for v in b:
                     buf = np.roll(buf, -1)
                     buf[-1] = v
@@ -238,7 +267,9 @@ class _WindowDecimate(Signal):
             up, cap, hop = self.up, self.cap, self.hop
 
             def gen():
-                s = _fft.Stft(cap, hop)
+                # rtl_tcp bytes go to the GPU as they are (converted in the frame load)
+                kind = _lib.CU8 if up.sample_kind == _lib.CU8 else _lib.C64
+                s = _fft.Stft(cap, hop, input_kind=kind)
                 for b in up.blocks():
                     y = s.process(b)
                     if y.shape[0]:
@@ -253,13 +284,41 @@ def fft(frames):
 
 
 # ---------------------------------------------------------------- sources
-def from_array(rate: float, x, block: int = DEFAULT_BLOCK) -> Signal:
+_LIBM = None
+
+
+def _polar_unit(ph: np.ndarray) -> np.ndarray:
+    """Complex::from_polar(&1.0, &ph) with glibc cosf / sinf -- what Rust's f32::cos / sin
+    call on Linux (numpy's float32 cos / sin differ from glibc by an ulp now and then)."""
+    import ctypes
+    global _LIBM
+    if _LIBM is None:
+        _LIBM = ctypes.CDLL("libm.so.6")
+        for fn in (_LIBM.cosf, _LIBM.sinf):
+            fn.restype = ctypes.c_float
+            fn.argtypes = [ctypes.c_float]
+    out = np.empty(ph.size, np.complex64)
+    for i, p in enumerate(ph.tolist()):
+        out[i] = complex(_LIBM.cosf(p), _LIBM.sinf(p))
+    return out
+
+def from_array(rate: float, x, block: int = DEFAULT_BLOCK,
+               sample_kind: Optional[int] = None) -> Signal:
+    """signal::from_iter (sources.rs:6-36) over an array, `block` samples per block.
+    sample_kind=CU8 marks x as raw rtl_tcp I/Q bytes (2 per sample), as RtlTcp.listen()
+    yields them."""
     x = np.asarray(x)
-    sk = _lib.C64 if np.iscomplexobj(x) else _lib.F32
+    sk = sample_kind if sample_kind is not None else (
+        _lib.C64 if np.iscomplexobj(x) else _lib.F32)
+    if sk == _lib.CU8:
+        x = np.ascontiguousarray(x, np.uint8).reshape(-1)
+        step = 2 * block
+    else:
+        step = block
 
     def gen():
-        for i in range(0, len(x), block):
-            yield x[i:i + block]
+        for i in range(0, len(x), step):
+            yield x[i:i + step]
     return Signal(rate, gen, sk)
 
 
@@ -269,13 +328,60 @@ def freq(rate: float, f: float, phase: float, n: int, block: int = DEFAULT_BLOCK
     dt = np.float32(1.0) / np.float32(rate)
     ff = np.float32(f)
     nph = np.float32(phase) / two_pi
-    out = np.empty(n, np.complex64)
+    phs = np.empty(n, np.float32)
     for i in range(n):
         nph = np.float32(nph + np.float32(dt * ff))
         nph = np.float32(nph - np.trunc(nph))
-        ph = np.float32(two_pi * nph)
-        out[i] = complex(np.cos(ph, dtype=np.float32), np.sin(ph, dtype=np.float32))
-    return from_array(rate, out, block)
+        phs[i] = np.float32(two_pi * nph)
+    return from_array(rate, _polar_unit(phs), block)
+
+
+def freq_sweep(rate: float, df: float, warmup: bool, start: float, end: float,
+               block: int = DEFAULT_BLOCK) -> Signal:
+    """signal::freq_sweep(rate, df, warmup, start..end) (sources.rs:181-194) through
+    FreqSweep::new / next (:129-174) in f32: blocks are records (freq, value) like the
+    reference's (f32, Complex<f32>) samples; the sweep ends after its length."""
+    f32 = np.float32
+    two_pi = f32(2.0) * f32(np.pi)
+    dfdt = f32(df) * f32(df)
+    if start > end:
+        dfdt = -dfdt
+    endt = (f32(end) - f32(start)) / dfdt
+    warmupt = f32(1.0) / f32(df) if warmup else f32(0.0)
+    fend_t = f32(warmupt + endt)
+
+    def as_usize(v):  # `(v * rate).round() as usize`: half away from zero, saturating
+        r = np.floor(np.abs(v) + 0.5) * np.sign(v)
+        return int(r) if r > 0 else 0
+    rate32 = f32(rate)
+    fstart = as_usize(f32(warmupt * rate32))
+    fend = as_usize(f32(fend_t * rate32))
+    n = fend
+    dt = f32(1.0) / rate32
+    fr = f32(start)
+    nph = f32(0.0) / two_pi
+    freqs = np.empty(n, np.float32)
+    phs = np.empty(n, np.float32)
+    for i in range(n):
+        d = dfdt
+        if fstart > 0:
+            fstart -= 1
+            d = f32(0.0)
+        if fend > 0:
+            fend -= 1
+        else:
+            d = f32(0.0)
+        fr = f32(fr + f32(dt * d))
+        nph = f32(nph + f32(dt * fr))
+        nph = f32(nph - np.trunc(nph))
+        phs[i] = f32(two_pi * nph)
+        freqs[i] = fr
+    rec = np.rec.fromarrays([freqs, _polar_unit(phs)], names="freq,value")
+
+    def gen():
+        for i in range(0, n, block):
+            yield rec[i:i + block]
+    return Signal(rate, gen, None)
 
 
 def impulse(rate: float, n: int, complex_: bool = False, block: int = DEFAULT_BLOCK) -> Signal:
