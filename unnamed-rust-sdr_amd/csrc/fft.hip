@@ -351,6 +351,126 @@ __global__ __launch_bounds__(16 * CB) void fft64k_pass_b(F64Args a) {
     }
 }
 
+
+// -------- one-pass radix-4 DIF for N = 4M, 8192 <= N <= 65536 (configs[2]'s 64 Ki frames) --
+// X[4k + m] = DFT_M(y_m)[k],  y_m[n] = (sum_p q_p[n] (-i)^{pm}) W_N^{mn},  q_p[n] = x[n + pM].
+// Workgroup (frame, m) computes one M-point transform (M <= 16384: 136 KiB padded LDS tile,
+// 1024 lanes x 16 points), reading the whole frame to form y_m in its load and writing every
+// 4th output bin.  No scratch slab and no inter-workgroup exchange: the four workgroups of a
+// frame share its input lines (and consecutive frames their overlap) through the XCD's L2,
+// and their interleaved plain stores merge into whole lines there before write-back.  Blocks
+// b, b+8, b+16, b+24 take the four m of one frame and each block group b % 8 a contiguous
+// range of frames -- on the round-robin XCD placement that keeps a frame (and its neighbours)
+// on one XCD (speed only; any placement gives the same results).
+struct Dif4Args {
+    FrameSrc src;
+    long nframes;
+    long fpg;           // frames per block group (ceil(nframes / 8))
+    const float2* twN;  // W_N, N entries
+    float norm;
+    int store_mode;
+    float2* out;
+};
+
+template <int R, int M, int NS, int NTH>
+__device__ __forceinline__ void dif4_pass(float2* lds, const float2* __restrict__ twN) {
+    constexpr int NBF = 16 / R;
+    constexpr int BPT = M / R;
+    const int t = threadIdx.x;
+    float2 v[NBF][R];
+#pragma unroll
+    for (int u = 0; u < NBF; ++u) {
+        const int j = t * NBF + u;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[u][r] = lds[fpad(j + r * BPT)];
+        if (NS > 1) {
+            const int k = j % NS;
+            twiddle<R, false>(v[u], twN, 4 * k * (M / (NS * R)));  // W_M^k = W_N^{4k}
+        }
+        Dft<R, false>::run(v[u]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NBF; ++u) {
+        const int j = t * NBF + u;
+        const int k = j % NS;
+        const int o = (j / NS) * NS * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[fpad(o + r * NS)] = v[u][r];
+    }
+    __syncthreads();
+}
+
+template <int M, int NS, int NTH>
+__device__ __forceinline__ void dif4_fft(float2* lds, const float2* __restrict__ twN) {
+    if constexpr (NS < M) {
+        constexpr int LEFT = M / NS;
+        constexpr int R = LEFT >= 16 ? 16 : LEFT;
+        dif4_pass<R, M, NS, NTH>(lds, twN);
+        dif4_fft<M, NS * R, NTH>(lds, twN);
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(M / 16) void fft_dif4_kernel(Dif4Args a) {
+    constexpr int NTH = M / 16;
+    constexpr long N = 4L * M;
+    extern __shared__ float2 dlds[];
+    const int t = threadIdx.x;
+    const long b = blockIdx.x;
+    const long g = b & 7, i = b >> 3;
+    const int m = (int)(i & 3);
+    const long f = g * a.fpg + (i >> 2);
+    if (f >= a.nframes) return;
+    const FrameSrc& s = a.src;
+    const float2* base = nullptr;  // fast path: the whole frame is contiguous in memory
+    if (s.mode == 0) base = s.in + f * N;
+    else if (s.mode == 1) {
+        const long g0 = s.first_end + f * s.hop - N;
+        if (g0 >= 0 && g0 + N <= s.n_in) base = s.in + g0;
+    }
+    // load + first radix-4 stage (output m only) + W_N^{mn}
+#pragma unroll 8
+    for (int q = 0; q < 16; ++q) {
+        const int n = t + NTH * q;
+        float2 x0, x1, x2, x3;
+        if (base) {
+            x0 = base[n];
+            x1 = base[n + M];
+            x2 = base[n + 2 * M];
+            x3 = base[n + 3 * M];
+        } else {
+            x0 = frame_sample(s, N, f, n);
+            x1 = frame_sample(s, N, f, n + M);
+            x2 = frame_sample(s, N, f, n + 2 * M);
+            x3 = frame_sample(s, N, f, n + 3 * M);
+        }
+        dft4<false>(x0, x1, x2, x3);
+        float2 y = m == 0 ? x0 : (m == 1 ? x1 : (m == 2 ? x2 : x3));
+        if (m) y = cmul(y, a.twN[m * n]);
+        dlds[fpad(n)] = y;
+    }
+    __syncthreads();
+    dif4_fft<M, 1, NTH>(dlds, a.twN);
+    // bin 4k + m of frame f
+    if (a.store_mode == 0) {
+        float2* O = a.out + f * N;
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int k = t + NTH * q;
+            const float2 x = dlds[fpad(k)];
+            const long o = (4L * k + m + N / 2) & (N - 1);
+            O[o] = make_float2(x.x * a.norm, x.y * a.norm);
+        }
+    } else {
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int k = t + NTH * q;
+            store_bin(a.out, f, N, 4L * k + m, dlds[fpad(k)], a.store_mode, a.norm);
+        }
+    }
+}
+
 }  // namespace
 
 // ------------------------------ plan / launch -------------------------------------------
@@ -433,9 +553,36 @@ void fft_plan_destroy(void* plan) {
 
 int fft_plan_size(void* plan) { return static_cast<FftPlanDev*>(plan)->M; }
 
+// one-pass radix-4 DIF sizes (no scratch slab): 8192 <= M <= 32768.  Measured for STFTs at
+// hop N/2 over 2^28 samples (profiles/r02_stft_dif4_ab.txt): 3.0-3.7 ms against 5.3-5.6 ms for
+// the generic four-step; at 65536 the one-pass form is latency-bound (one 139 KiB workgroup
+// per CU, phases serialised: 4.1 ms) and the dedicated 64K two-pass path below wins (2.2 ms).
+static bool use_dif4(int M) { return M >= 8192 && M <= 32768; }
+
 static size_t frame_scratch_bytes(const FftPlanDev* p) {
     if (p->gen) return fftgen_frame_scratch_bytes(p->gen);
-    return p->M <= kTile ? 0 : (size_t)p->M * sizeof(float2);
+    return (p->M <= kTile || use_dif4(p->M)) ? 0 : (size_t)p->M * sizeof(float2);
+}
+
+template <int MQ>
+static int launch_dif4(const FftPlanDev* p, const FrameSrc& src, long nframes, float2* out,
+                       int store_mode, hipStream_t s) {
+    constexpr size_t lds = (size_t)(MQ + MQ / 16) * sizeof(float2);
+    static const bool attr = hipFuncSetAttribute((const void*)fft_dif4_kernel<MQ>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds) == hipSuccess;
+    if (!attr) return SDRGPU_ERR_LAUNCH;
+    Dif4Args a{};
+    a.src = src;
+    a.nframes = nframes;
+    a.fpg = (nframes + 7) / 8;
+    a.twN = p->twM;
+    a.norm = p->norm;
+    a.store_mode = store_mode;
+    a.out = out;
+    hipLaunchKernelGGL(fft_dif4_kernel<MQ>, dim3((unsigned)(32 * a.fpg)), dim3(MQ / 16), lds, s, a);
+    SDRGPU_LAUNCH_CHECK();
+    return SDRGPU_OK;
 }
 
 size_t fft_scratch_bytes(void* plan) {
@@ -498,6 +645,13 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         }
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
+    }
+    if (use_dif4(p->M)) {
+        switch (p->M) {
+        case 8192: return launch_dif4<2048>(p, src, fr.nframes, out, store_mode, s);
+        case 16384: return launch_dif4<4096>(p, src, fr.nframes, out, store_mode, s);
+        default: return launch_dif4<8192>(p, src, fr.nframes, out, store_mode, s);
+        }
     }
     if (!scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
     static const bool use64 = [] {

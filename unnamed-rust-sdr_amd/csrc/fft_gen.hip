@@ -300,8 +300,9 @@ struct BluArgs {
     long nframes;
     int N, M;
     const float2* chirp;  // w[n] = e^{-i pi n^2 / N}, N entries
-    const float2* bhat;   // conj(FFT_M(b)) / M ... see blu_mid
+    const float2* bhat;   // FFT_M(b) / M, see blu_mid
     float2* T;            // nframes x M work frames
+    float2* U;            // a second nframes x M set (the power-of-two kernels run out of place)
     float norm;
     int store_mode;
     float2* out;
@@ -317,14 +318,14 @@ __global__ void blu_pre(BluArgs a) {
     }
 }
 
-// T = conj(FFT(a) * Bh) with Bh = FFT_M(b) / M: the next forward transform then gives
-// conj(M * IFFT(FFT(a) Bh)) = conj(a (*) b) (circular convolution of length M)
+// T = conj(U * Bh) with U = FFT(a) and Bh = FFT_M(b) / M: the next forward transform then
+// gives conj(M * IFFT(FFT(a) Bh)) = conj(a (*) b) (circular convolution of length M)
 __global__ void blu_mid(BluArgs a) {
     const long total = a.nframes * (long)a.M;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
          i += (long)gridDim.x * blockDim.x) {
         const int m = (int)(i % a.M);
-        a.T[i] = conjf2(cmul(a.T[i], a.bhat[m]));
+        a.T[i] = conjf2(cmul(a.U[i], a.bhat[m]));
     }
 }
 
@@ -334,7 +335,7 @@ __global__ void blu_post(BluArgs a) {
          i += (long)gridDim.x * blockDim.x) {
         const long f = i / a.N;
         const int k = (int)(i - f * a.N);
-        const float2 c = conjf2(a.T[f * a.M + k]);
+        const float2 c = conjf2(a.U[f * a.M + k]);
         store_bin(a.out, f, a.N, k, cmul(a.chirp[k], c), a.store_mode, a.norm);
     }
 }
@@ -488,8 +489,8 @@ void* fftgen_plan_create(int N, int* status) {
 size_t fftgen_frame_scratch_bytes(void* plan) {
     auto* p = static_cast<GenFftPlan*>(plan);
     if (p->kind == kFourKind) return (size_t)p->N * sizeof(float2);
-    if (p->kind == kBluKind)
-        return (size_t)p->M * sizeof(float2) * (fft_scratch_frames(p->inner) ? 2 : 1);
+    if (p->kind == kBluKind)  // T and U, plus the inner plan's own slab if it has one
+        return (size_t)p->M * sizeof(float2) * (fft_scratch_frames(p->inner) ? 3 : 2);
     return 0;
 }
 
@@ -561,16 +562,19 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         }
         return SDRGPU_OK;
     }
-    // Bluestein: per batch, T (nf x M) then (if the inner plan needs one) its own scratch
+    // Bluestein: per batch T and U (nf x M each), then (if the inner plan needs one) its slab;
+    // every transform runs T -> U (the power-of-two kernels are not in place)
     const long M = p->M;
     const bool inner_scratch = fft_scratch_frames(p->inner) != 0;
-    float2* inner_buf = inner_scratch ? scratch + (long)scratch_frames * M : nullptr;
+    float2* U = scratch + (long)scratch_frames * M;
+    float2* inner_buf = inner_scratch ? scratch + 2L * (long)scratch_frames * M : nullptr;
     BluArgs a{};
     a.N = (int)N;
     a.M = (int)M;
     a.chirp = p->chirp;
     a.bhat = p->bhat;
     a.T = scratch;
+    a.U = U;
     a.norm = p->norm;
     a.store_mode = store_mode;
     for (long f0 = 0; f0 < fr.nframes; f0 += (long)scratch_frames) {
@@ -586,11 +590,11 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         in.mode = 0;
         in.in = scratch;
         in.nframes = nf;
-        int st = fft_launch(p->inner, in, scratch, 2, inner_buf, inner_scratch ? scratch_frames : 0, s);
+        int st = fft_launch(p->inner, in, U, 2, inner_buf, inner_scratch ? scratch_frames : 0, s);
         if (st) return st;
         hipLaunchKernelGGL(blu_mid, dim3(g), dim3(256), 0, s, a);
         SDRGPU_LAUNCH_CHECK();
-        if ((st = fft_launch(p->inner, in, scratch, 2, inner_buf, inner_scratch ? scratch_frames : 0, s)))
+        if ((st = fft_launch(p->inner, in, U, 2, inner_buf, inner_scratch ? scratch_frames : 0, s)))
             return st;
         const unsigned gp = (unsigned)std::min<long>(4096, (nf * N + 255) / 256);
         hipLaunchKernelGGL(blu_post, dim3(gp), dim3(256), 0, s, a);
