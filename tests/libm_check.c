@@ -23,6 +23,9 @@ static void* run_trig(void* a) {
             sdr_sincosf_bf(x, &bs, &bc); /* branch-free GPU form */
             if (sdr_asuint(rs) != sdr_asuint(bs)) j->mis++;
             if (sdr_asuint(rc) != sdr_asuint(bc)) j->mis++;
+            sdr_sincosf_bf2(x, &bs, &bc); /* sign-after-evaluation form (the kernel's) */
+            if (sdr_asuint(rs) != sdr_asuint(bs)) j->mis++;
+            if (sdr_asuint(rc) != sdr_asuint(bc)) j->mis++;
         }
     return 0;
 }
@@ -44,10 +47,34 @@ static void* run_atan2(void* a) {
                  x = y * (1.0f + ((float)((int32_t)(xs(&s) >> 40)) / 8388608.0f) * 1e-3f); break;
         }
         float a1 = atan2f(y, x), a2 = sdr_atan2f(y, x), a3 = sdr_atan2f_bf(y, x);
+        float a4 = sdr_atan2f_bfx(y, x);
         if (sdr_asuint(a1) != sdr_asuint(a2) && !(isnan(a1) && isnan(a2))) j->mis++;
         if (sdr_asuint(a1) != sdr_asuint(a3) && !(isnan(a1) && isnan(a3))) j->mis++;
+        if (sdr_asuint(a1) != sdr_asuint(a4) && !(isnan(a1) && isnan(a4))) j->mis++;
     }
     return 0;
+}
+
+/* every pair of special / boundary values (zeros, infinities, NaN, 1, tiny / huge, the
+ * |k| = 60 boundary, denormals) through the fully branch-free atan2f */
+static long special_pairs(void) {
+    const float v[] = {0.0f, 1.0f, 2.0f, 0.5f, 3.0f, 1e-30f, 1e30f, 1e-45f, 1.17549435e-38f,
+                       3.4028235e38f, INFINITY, NAN, 0x1p60f, 0x1p61f, 0x1p-60f, 0x1p-61f,
+                       0x1p25f, 0x1p-29f, 0.4375f, 0.6875f, 1.1875f, 2.4375f, 1.0000001f,
+                       0.99999994f, 7.0f, 1e-7f};
+    const int nv = sizeof v / sizeof v[0];
+    long mis = 0;
+    for (int i = 0; i < nv; ++i)
+        for (int j = 0; j < nv; ++j)
+            for (int s = 0; s < 4; ++s) {
+                const float y = (s & 1) ? -v[i] : v[i], x = (s & 2) ? -v[j] : v[j];
+                const float a1 = atan2f(y, x), a4 = sdr_atan2f_bfx(y, x);
+                if (sdr_asuint(a1) != sdr_asuint(a4) && !(isnan(a1) && isnan(a4))) {
+                    if (mis < 10) printf("atan2f(%a, %a): glibc %a, bfx %a\n", y, x, a1, a4);
+                    mis++;
+                }
+            }
+    return mis;
 }
 
 int main(int argc, char** argv) {
@@ -68,6 +95,8 @@ int main(int argc, char** argv) {
         pthread_create(&th[t], 0, run_atan2, &jb[t]);
     }
     for (int t = 0; t < T; ++t) { pthread_join(th[t], 0); ma += jb[t].mis; }
-    printf("sinf/cosf |x|<%g: %ld mismatches; atan2f %ld pairs: %ld mismatches\n", limit, mt, npairs, ma);
-    return (mt || ma) ? 1 : 0;
+    const long ms = special_pairs();
+    printf("sinf/cosf |x|<%g: %ld mismatches; atan2f %ld pairs: %ld mismatches; special pairs: %ld\n",
+           limit, mt, npairs, ma, ms);
+    return (mt || ma || ms) ? 1 : 0;
 }

@@ -252,6 +252,35 @@ SDR_LIBM_FN float sdr_atan2f(float y, float x) {
  *    |y/x| beyond 2^+-60, x == 1) fall back to the reference function.
  * Validated bit-exact against the host libm by tests/test_libm_restatement.py.
  * ------------------------------------------------------------------------------------- */
+/* As sdr_sincosf_bf with fewer instructions: both polynomials are odd/even in a way that
+ * makes the sign handling exact AFTER evaluation -- sin_poly(-x) = -sin_poly(x) and the
+ * negated-coefficient cosine table gives exactly -cos_poly (every fma / mul / add of the
+ * evaluation commutes with negation under round-to-nearest) -- so one positive-coefficient
+ * evaluation of each and a sign flip of the f32 results replace the f64 selects. */
+SDR_LIBM_FN void sdr_sincosf_bf2(float y, float* sinp, float* cosp) {
+    int n;
+    const double xr = sdr_reduce_fast((double)y, &n);
+    const double x2 = xr * xr;
+    const double x3 = xr * x2;
+    const double s1 = SDR_MAD(x2, SDR_S3, SDR_S2);
+    const double x7 = x3 * x2;
+    const double ss = SDR_MAD(x3, SDR_S1, xr);
+    const float sp0 = (float)SDR_MAD(x7, s1, ss);         /* sin_poly(xr) */
+    const double x4 = x2 * x2;
+    const double c2 = SDR_MAD(x2, SDR_C4, SDR_C3);
+    const double c1 = SDR_MAD(x2, SDR_C1, 1.0);
+    const double x6 = x4 * x2;
+    const double cc = SDR_MAD(x4, SDR_C2, c1);
+    const float cp0 = (float)SDR_MAD(x6, c2, cc);         /* cos_poly(xr), table[0] */
+    const uint32_t sgn_s = (((n & 3) == 1) | ((n & 3) == 2)) ? 0x80000000u : 0u;
+    const uint32_t sgn_c = (n & 2) ? 0x80000000u : 0u;
+    const float sp = sdr_asfloat(sdr_asuint(sp0) ^ sgn_s);
+    const float cp = sdr_asfloat(sdr_asuint(cp0) ^ sgn_c);
+    const int tiny = sdr_abstop12(y) < 0x398; /* |y| < 2^-12: sinf returns y, cosf 1 */
+    *sinp = tiny ? y : ((n & 1) ? cp : sp);
+    *cosp = tiny ? 1.0f : ((n & 1) ? sp : cp);
+}
+
 SDR_LIBM_FN void sdr_sincosf_bf(float y, float* sinp, float* cosp) {
     int n;
     const double xr = sdr_reduce_fast((double)y, &n);
@@ -332,6 +361,47 @@ SDR_LIBM_FN float sdr_atan2f_bf(float y, float x) {
     const float r2 = pi - t, r3 = t - pi;
     const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
     return m == 0 ? z : m == 1 ? r1 : m == 2 ? r2 : r3;
+}
+
+/* Fully branch-free atan2f: the reference's special cases (e_atan2f.c) as selects of
+ * constants instead of a fallback call, so a wave never runs -- or carries the code of -- the
+ * reference function.  Order of the reference's checks: NaN; x == 1 (atanf(y): the common
+ * path gives the same bits, atanf being exactly odd in fdlibm); y == 0; x == 0; x = inf;
+ * y = inf; |y/x| beyond 2^60 (z = pi/2 + pi_lo/2) or below 2^-60 with x < 0 (z = 0); else
+ * z = atanf(|y/x|); then the quadrant from the signs. */
+SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
+    const float tiny = 1.0e-30f, zero = 0.0f;
+    const float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f;
+    const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)sdr_asuint(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)sdr_asuint(y), iy = hy & 0x7fffffff;
+    const int32_t k = (iy - ix) >> 23;
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    /* common path (its value is discarded wherever a special case applies) */
+    const float qq = y / x;
+    const float za = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
+    const float z = k > 60 ? pi_o_2 + (float)0.5 * pi_lo : ((hx < 0) & (k < -60)) ? 0.0f : za;
+    const float t = z - pi_lo;
+    const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
+    const float gen = m == 0 ? z : m == 1 ? r1 : m == 2 ? pi - t : t - pi;
+    /* special cases, reference order (later checks apply only where earlier ones did not) */
+    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
+    const float half = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;                  /* x == 0, y = inf */
+    const float infinf = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny
+                       : m == 2 ? (float)3.0 * pi_o_4 + tiny : (float)-3.0 * pi_o_4 - tiny;
+    const float inffin = m == 0 ? zero : m == 1 ? -zero : m == 2 ? pi + tiny : -pi - tiny;
+    float r = gen;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* a wave skips the special-case selects when none of its lanes needs them */
+    const int spec = (iy >= 0x7f800000) | (ix >= 0x7f800000) | (ix == 0) | (iy == 0);
+    if (!__builtin_amdgcn_ballot_w64(spec)) return r;
+#endif
+    r = (iy == 0x7f800000) ? half : r;
+    r = (ix == 0x7f800000) ? ((iy == 0x7f800000) ? infinf : inffin) : r;
+    r = (ix == 0) ? half : r;
+    r = (iy == 0) ? by_m_pi : r;
+    r = ((ix > 0x7f800000) | (iy > 0x7f800000)) ? x + y : r;
+    return r;
 }
 
 #endif /* SDR_LIBM_GLIBC_H */

@@ -8,8 +8,10 @@
 // out_mode 1 writes the stereo difference signal of src/main.rs:58-66 instead of `out`.
 //
 // The recurrence is serial and nonlinear (atan2 -> NCO -> sin/cos each sample), so it is
-// latency-bound, not HBM- or FLOP-bound; the next 8 samples of every lane
-// are in flight while the current 8 are processed.
+// latency-bound, not HBM- or FLOP-bound: a channel costs the issue of its
+// per-sample instruction stream (one wave per SIMD at 1024 channels), so every instruction
+// off the recurrence counts; the next 8 samples of every lane are in flight while the
+// current 8 are processed.
 //
 // Bit-exact by construction: on noisy input the reference loop is chaotic (a 1-ulp change
 // in one sample moves the next cycle slip; FMA vs no-FMA builds of the same code differ by
@@ -18,6 +20,7 @@
 // Mul, Biquad::apply's `0 + v*b0 + x1*b1 + ...`), and sin/cos/atan2 are the bit-exact
 // restatements of the glibc functions Rust std calls (libm_glibc.h).
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "libm_glibc.h"
@@ -51,8 +54,15 @@ __device__ __forceinline__ float bq_real(const Bq& c, float x, float& x1, float&
 }
 
 // U8: samples are rtl_tcp byte pairs, converted as RtlTcpSignal::next does
-// ((v as f32 - 128.0) / 128.0, src/rtltcp.rs:156-164 -- exact in f32) inside the load
-template <bool U8>
+// ((v as f32 - 128.0) / 128.0, src/rtltcp.rs:156-164 -- exact in f32) inside the load.
+// LID / OID / KID: loop / output / lock filter is Identity (1), a biquad (0) or read from the
+// parameters at run time (2); MODE: output mode 0 / 1, or 2 = run time.  The designs of the
+// reference's callers are compiled as their own kernels (src/main.rs:41-46: loop LowPass,
+// output Identity, lock LowPass; examples/pll.rs:9-15: three LowPass; the stereo pilot
+// src/main.rs:55-60), so no per-sample control flow is left in them.
+// VEC: the channel's rows are 16-B aligned with ld_in even / ld_out a multiple of 8, so a
+// chunk of 8 samples moves in 4 (c64) or 1 (u8) loads and 3 stores.
+template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
 __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const void* __restrict__ in_,
                                                         long ld_in, long n, float* __restrict__ out,
                                                         uint8_t* __restrict__ locked, long ld_out,
@@ -62,20 +72,22 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
     PllChannelState s = state[ch];
     const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;
     const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;
+    auto cvt = [](unsigned w) -> float2 {
+        return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);
+    };
     auto ld = [&](long i) -> float2 {
-        if constexpr (U8) {
-            const unsigned w = xu[i];
-            return make_float2(((float)(w & 255u) - 128.0f) / 128.0f,
-                               ((float)(w >> 8) - 128.0f) / 128.0f);
-        } else {
-            return xf[i];
-        }
+        if constexpr (U8) return cvt(xu[i]);
+        else return xf[i];
     };
     float* __restrict__ y = out + ch * ld_out;
     uint8_t* __restrict__ lk = locked + ch * ld_out;
     const Bq L = {p.loopc[0], p.loopc[1], p.loopc[2], p.loopc[3], p.loopc[4]};
     const Bq O = {p.outc[0], p.outc[1], p.outc[2], p.outc[3], p.outc[4]};
     const Bq K = {p.lockc[0], p.lockc[1], p.lockc[2], p.lockc[3], p.lockc[4]};
+    const bool loop_id = LID == 2 ? p.loop_ident != 0 : LID == 1;
+    const bool out_id = OID == 2 ? p.out_ident != 0 : OID == 1;
+    const bool lock_id = KID == 2 ? p.lock_ident != 0 : KID == 1;
+    const int mode = MODE == 2 ? p.out_mode : MODE;
     constexpr float kTwoPi = 2.0f * 3.14159265358979323846f;  // 2.0 * f32::consts::PI
 
     // one reference Pll::apply step; returns (output or 0, locked)
@@ -85,7 +97,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         const float cr = v.x * cjr - v.y * cji;
         const float ci = v.x * cji + v.y * cjr;
         float lr = cr, li = ci;
-        if (!p.loop_ident) {
+        if (!loop_id) {
             // Biquad<f32, Complex<f32>>::apply: Convolve::accumulate = out += a * c
             float orr = 0.0f, oi = 0.0f;
             orr += cr * L.b0;      oi += ci * L.b0;
@@ -98,20 +110,22 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
             lr = orr;
             li = oi;
         }
-        const float phasedif = sdr_atan2f_bf(li, lr) * p.gain;    // :72 arg() * gain
+        const float phasedif = sdr_atan2f_bfx(li, lr) * p.gain;   // :72 arg() * gain
         float nph = s.nphase + (p.reference + phasedif);           // :73
         nph = nph - truncf(nph);                                   // :74 fract()
         s.nphase = nph;
         const float phase = kTwoPi * nph;                          // :75
         float sn, cs;
-        sdr_sincosf_bf(phase, &sn, &cs);                           // glibc sinf/cosf, branch-free
+        sdr_sincosf_bf2(phase, &sn, &cs);                          // glibc sinf/cosf, branch-free
         s.vr = 1.0f * cs;                                          // :76 from_polar
         s.vi = 1.0f * sn;
-        const float lockv = p.lock_ident ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
-        const float o = p.out_ident ? phasedif * p.rate
-                                    : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
+        // off the loop-carried chain: lock / output filters and the output select
+        const float lockv = lock_id ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
+        const float o = out_id ? phasedif * p.rate
+                               : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
         const bool lockd = lockv > 0.01f;                          // :80
-        if (p.out_mode == 1) {
+        lv = lockd ? 1 : 0;
+        if (mode == 1) {
             // src/main.rs:58-66, the stereo pilot: input = Complex::new(v, 0.0);
             // diff = (v / value.powi(2)).re * 0.5 when locked.  powi(2) = value * value
             // (num-complex Mul); f32 / Complex: re = v * w.re / norm_sqr(w)
@@ -120,36 +134,69 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
             const float nrm = wr * wr + wi * wi;
             const float dre = v.x * wr / nrm;
             ov = lockd ? dre * 0.5f : 0.0f;
-            lv = lockd ? 1 : 0;
-            return;
+        } else {
+            ov = lockd ? o : 0.0f;
         }
-        ov = lockd ? o : 0.0f;
-        lv = lockd ? 1 : 0;
     };
 
     // full chunks of kChunk samples, the next chunk's loads in flight
+    using RawT = std::conditional_t<U8, uint4, float4>;
+    constexpr int NR = U8 ? 1 : kChunk / 2;  // raw vector loads per chunk
     const long nfull = n / kChunk * kChunk;
+    RawT raw[NR];
+    auto ldc = [&](long i) {  // chunk starting at sample i
+        if constexpr (VEC) {
+            const RawT* q = reinterpret_cast<const RawT*>(U8 ? (const void*)(xu + i) : (const void*)(xf + i));
+#pragma unroll
+            for (int r = 0; r < NR; ++r) raw[r] = q[r];
+        }
+    };
+    auto sample = [&](int k, long i) -> float2 {
+        if constexpr (VEC) {
+            if constexpr (U8) {
+                const unsigned w = (&raw[0].x)[k >> 1];
+                return cvt((k & 1) ? (w >> 16) : (w & 0xffffu));
+            } else {
+                const float4 r = raw[k >> 1];
+                return (k & 1) ? make_float2(r.z, r.w) : make_float2(r.x, r.y);
+            }
+        } else {
+            return ld(i + k);
+        }
+    };
     float2 buf[kChunk];
     if (nfull > 0) {
+        ldc(0);
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) buf[k] = ld(k);
+        for (int k = 0; k < kChunk; ++k) buf[k] = sample(k, 0);
     }
     for (long i = 0; i < nfull; i += kChunk) {
         float2 cur[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) cur[k] = buf[k];
-        if (i + kChunk < nfull) {
+        if (i + kChunk < nfull) {  // prefetch
+            ldc(i + kChunk);
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) buf[k] = ld(i + kChunk + k);  // prefetch
+            for (int k = 0; k < kChunk; ++k) buf[k] = sample(k, i + kChunk);
         }
         float ov[kChunk];
         uint8_t lv[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) step(cur[k], ov[k], lv[k]);
+        if constexpr (VEC) {
+            float4* yo = reinterpret_cast<float4*>(y + i);
+            yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+            yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
+            uint2 pk;
+            pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
+            pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
+            *reinterpret_cast<uint2*>(lk + i) = pk;
+        } else {
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            y[i + k] = ov[k];
-            lk[i + k] = lv[k];
+            for (int k = 0; k < kChunk; ++k) {
+                y[i + k] = ov[k];
+                lk[i + k] = lv[k];
+            }
         }
     }
     // ragged tail: exactly n - nfull more samples (the state must not see padding)
@@ -163,18 +210,43 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
     state[ch] = s;
 }
 
+template <bool U8, int LID, int OID, int KID, int MODE>
+void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
+                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
+    const long nblk = (p.nch + kPllBlock - 1) / kPllBlock;
+    const size_t sb = U8 ? 2 : 8;
+    const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in * sb) % 16 == 0 &&
+                     (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (ld_out % 8) == 0 &&
+                     (reinterpret_cast<uintptr_t>(locked) & 7) == 0;
+    if (vec)
+        hipLaunchKernelGGL((pll_kernel<U8, LID, OID, KID, MODE, true>), dim3((unsigned)nblk),
+                           dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
+    else
+        hipLaunchKernelGGL((pll_kernel<U8, LID, OID, KID, MODE, false>), dim3((unsigned)nblk),
+                           dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
+}
+
+template <bool U8>
+void launch_any(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
+                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
+    const int l = p.loop_ident, o = p.out_ident, k = p.lock_ident, m = p.out_mode;
+    if (!l && o && !k && m == 0)            // src/main.rs:41-46
+        launch_cfg<U8, 0, 1, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, s);
+    else if (!l && !o && !k && m == 0)      // examples/pll.rs:9-15
+        launch_cfg<U8, 0, 0, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, s);
+    else if (!l && !o && !k && m == 1)      // the stereo pilot, src/main.rs:55-66
+        launch_cfg<U8, 0, 0, 0, 1>(p, in, ld_in, n, out, locked, ld_out, state, s);
+    else
+        launch_cfg<U8, 2, 2, 2, 2>(p, in, ld_in, n, out, locked, ld_out, state, s);
+}
+
 }  // namespace
 
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
     if (n <= 0) return SDRGPU_OK;
-    const long nblk = (p.nch + kPllBlock - 1) / kPllBlock;
-    if (p.in_u8)
-        hipLaunchKernelGGL(pll_kernel<true>, dim3((unsigned)nblk), dim3(kPllBlock), 0, s, p, in,
-                           ld_in, n, out, locked, ld_out, state);
-    else
-        hipLaunchKernelGGL(pll_kernel<false>, dim3((unsigned)nblk), dim3(kPllBlock), 0, s, p, in,
-                           ld_in, n, out, locked, ld_out, state);
+    if (p.in_u8) launch_any<true>(p, in, ld_in, n, out, locked, ld_out, state, s);
+    else launch_any<false>(p, in, ld_in, n, out, locked, ld_out, state, s);
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }
