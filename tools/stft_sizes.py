@@ -1,4 +1,4 @@
-# STFT throughput per frame size (hop N/2, 2^28 c64 zeros resident): python tools/stft_sizes.py
+# STFT throughput per frame size (hop N/2, 2^28 c64 zeros resident): python tools/stft_sizes.py [N ...]
 import sys, os, json, time
 sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"] + "/unnamed-rust-sdr_amd")
 import numpy as np, sdrgpu
@@ -6,7 +6,8 @@ from sdrgpu.device import DeviceBuffer, Event, synchronize
 n_in = 1 << 28
 x = DeviceBuffer.empty(n_in)
 x.fill_zero()
-for N in (8192, 16384, 32768, 65536):
+SIZES = [int(v) for v in sys.argv[1:]] or [8192, 16384, 32768, 65536]
+for N in SIZES:
     st = sdrgpu.fft.Stft(N, N // 2)
     nf = st.output_len(n_in)
     y = DeviceBuffer.empty(nf * N)
