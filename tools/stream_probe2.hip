@@ -67,6 +67,89 @@ __global__ __launch_bounds__(512) void k_vgpr(const f32x4* __restrict__ in, f32x
     }
 }
 
+// register streaming, COOP: the workgroup shares one contiguous range (wave w takes tiles
+// w, w+W, ...); HIST: each tile also re-reads the 256 samples before it (the FIR history a
+// wave would need when its tiles are not adjacent; L2 hits when the neighbour loaded them)
+template <int DEPTH, bool HIST>
+__global__ __launch_bounds__(512) void k_vgpr_coop(const f32x4* __restrict__ in, f32x4* __restrict__ out,
+                                                  long ntiles) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, W = blockDim.x >> 6;
+    const long b0 = blockIdx.x * ntiles / gridDim.x, b1 = (blockIdx.x + 1) * ntiles / gridDim.x;
+    const long t0 = b0 + wv;
+    constexpr int NL = HIST ? 10 : 8;
+    f32x4 buf[DEPTH][NL];
+    auto ld = [&](f32x4 (&b)[NL], long t) {
+        const long tt = t < b1 ? t : t0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = __builtin_nontemporal_load(in + tt * kTileF4 + 64 * k + lane);
+        if (HIST) {
+            const long th = tt > 0 ? tt : 1;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) b[8 + k] = in[th * kTileF4 - 128 + 64 * k + lane];
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) ld(buf[d], t0 + d * W);
+    for (long t = t0; t < b1; t += DEPTH * W) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long tc = t + d * W;
+            if (tc >= b1) break;
+            f32x4 a = buf[d][0] + buf[d][1] + buf[d][2] + buf[d][3];
+            f32x4 b = buf[d][4] + buf[d][5] + buf[d][6] + buf[d][7];
+            if (HIST) a += buf[d][8] + buf[d][9];
+            ld(buf[d], tc + DEPTH * W);
+            f32x4* o = out + tc * 128 + 2 * lane;
+            __builtin_nontemporal_store(a, o);
+            __builtin_nontemporal_store(b, o + 1);
+        }
+    }
+}
+
+// register streaming in RUNS: the workgroup's range is cut into runs of L tiles; wave w takes
+// runs w, w+W, ... (so the CU's waves work on W adjacent runs at a time) and re-reads the
+// 256 samples before each run (history); prefetch crosses run boundaries
+template <int DEPTH>
+__global__ __launch_bounds__(512) void k_vgpr_runs(const f32x4* __restrict__ in, f32x4* __restrict__ out,
+                                                  long ntiles, int L) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, W = blockDim.x >> 6;
+    const long b0 = blockIdx.x * ntiles / gridDim.x, b1 = (blockIdx.x + 1) * ntiles / gridDim.x;
+    // k-th tile of this wave: run (k / L) * W + wv, tile k % L inside it
+    auto tile_of = [&](long k) { return b0 + ((k / L) * W + wv) * L + (k % L); };
+    f32x4 buf[DEPTH][10];
+    auto ld = [&](f32x4 (&b)[10], long k) {
+        long tt = tile_of(k);
+        const bool ok = tt < b1;
+        tt = ok ? tt : b0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[q] = __builtin_nontemporal_load(in + tt * kTileF4 + 64 * q + lane);
+        if ((k % L) == 0) {
+            const long th = tt > 0 ? tt : 1;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) b[8 + q] = in[th * kTileF4 - 128 + 64 * q + lane];
+        } else {
+            b[8] = b[9] = f32x4{0, 0, 0, 0};
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) ld(buf[d], d);
+    for (long k = 0;; k += DEPTH) {
+        bool done = false;
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const long tc = tile_of(k + d);
+            if (tc >= b1) { done = true; break; }
+            f32x4 a = buf[d][0] + buf[d][1] + buf[d][2] + buf[d][3] + buf[d][8];
+            f32x4 b = buf[d][4] + buf[d][5] + buf[d][6] + buf[d][7] + buf[d][9];
+            ld(buf[d], k + d + DEPTH);
+            f32x4* o = out + tc * 128 + 2 * lane;
+            __builtin_nontemporal_store(a, o);
+            __builtin_nontemporal_store(b, o + 1);
+        }
+        if (done) break;
+    }
+}
+
 // LDS-DMA streaming: per-wave ring of RING tiles (8 KiB each) in LDS; tile t+RING is issued
 // right after tile t is consumed; counted vmcnt (stores count too: 2 stores + 8 DMAs per tile)
 // COOP: the workgroup's waves share one contiguous range (wave w takes tiles w, w+W, ...):
@@ -161,6 +244,27 @@ int main() {
         timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL(k_vgpr<1>, dim3(cus), dim3(64 * wpc), 0, 0, in, out, ntiles); });
         snprintf(nm, sizeof nm, "vgpr d2 %d waves/CU", wpc);
         timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL(k_vgpr<2>, dim3(cus), dim3(64 * wpc), 0, 0, in, out, ntiles); });
+    }
+    for (int wpc : {4, 8}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "vgpr coop d1 %d waves/CU", wpc);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_coop<1, false>), dim3(cus), dim3(64 * wpc), 0, 0, in, out, ntiles); });
+        snprintf(nm, sizeof nm, "vgpr coop d2 %d waves/CU", wpc);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_coop<2, false>), dim3(cus), dim3(64 * wpc), 0, 0, in, out, ntiles); });
+        snprintf(nm, sizeof nm, "vgpr coop+hist d1 %d waves/CU", wpc);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_coop<1, true>), dim3(cus), dim3(64 * wpc), 0, 0, in, out, ntiles); });
+    }
+    for (int L : {1, 2, 4, 8, 16, 32}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "vgpr runs L=%d d1 8w", L);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_runs<1>), dim3(cus), dim3(512), 0, 0, in, out, ntiles, L); });
+    }
+    for (int L : {4, 8, 16}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "vgpr runs L=%d d2 8w", L);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_runs<2>), dim3(cus), dim3(512), 0, 0, in, out, ntiles, L); });
+        snprintf(nm, sizeof nm, "vgpr runs L=%d d2 4w", L);
+        timeit(nm, 10.0 * n, [&] { hipLaunchKernelGGL((k_vgpr_runs<2>), dim3(cus), dim3(256), 0, 0, in, out, ntiles, L); });
     }
     timeit("vgpr d2 2x8 waves/CU", 10.0 * n, [&] { hipLaunchKernelGGL(k_vgpr<2>, dim3(2 * cus), dim3(512), 0, 0, in, out, ntiles); });
     timeit("write-only default", 2.0 * n, [&] { hipLaunchKernelGGL(k_write_def, dim3(4096), dim3(256), 0, 0, out, n4 / 4); });

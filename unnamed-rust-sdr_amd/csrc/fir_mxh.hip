@@ -5,8 +5,8 @@
 // src/filter/convolve.rs:13-15, src/signal/adapters/mod.rs:30-37) for complex samples and
 // real taps: y[m] = sum_k h[k] x[i0 + 4m - k], zero history before the stream start.
 //
-// Same GEMM shape, tiles and conflict-free LDS swizzle as fir_mxl.hip (read that header
-// first); what changes is the operand format, which halves both the MFMA work and the
+// Same GEMM shape, tiles and conflict-free LDS swizzle as the exact bf16x3 variant kept in
+// tools/experiments/fir_mxl.hip (read that header first); what changes is the operand format, which halves both the MFMA work and the
 // LDS footprint so that two waves share each SIMD (one's VALU/LDS staging and memory waits
 // overlap the other's MFMAs):
 //   * every tile's window (1024 new samples + H history samples) is staged with its own
@@ -41,13 +41,19 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kTileOut = 256;
 constexpr int kWaves = 8;               // two waves per SIMD
 constexpr int kBlock = 64 * kWaves;
+// D = 1 tiles: three 256-output column sets share one staged window (2.48 vs 2.62 ms with one
+// set at configs[4]; profiles/r02_fir_d1_cs.txt), and 6 groups keep one raw tile in flight
+constexpr int kCs1 = 3;
+constexpr int kRunTiles = 8;
 
-template <int NCH, int D = 4>
+// CS: 256-output MFMA column sets per tile.  D = 1 stages the window's history once for CS
+// column sets (the history is 1.5x a 256-sample set, so re-staging it per set dominated)
+template <int NCH, int D = 4, int CS = 1>
 struct GeoH {
-    static constexpr int TI = 256 * D;             // new samples per tile (256 outputs)
+    static constexpr int TO = 256 * CS;            // outputs per tile
+    static constexpr int TI = TO * D;              // new samples per tile
     static constexpr int HR = 32 * NCH - 16 * D;   // history samples a tile's windows need
     static constexpr int H = (HR + 127) / 128 * 128;  // staged history (128-sample groups)
     static constexpr int OFF = H - HR;             // window offset inside the buffer
@@ -77,6 +83,7 @@ struct MxhParams {
     long ld_out;
     long tpc, spc, seg_tiles, units;
     int vec_out;
+    int blocked;  // units in per-workgroup contiguous ranges, wave w takes units w, w+8, ...
 };
 
 __device__ __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, f32x4 c) {
@@ -201,11 +208,11 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // 2 MFMAs per component per chunk.
 // D: decimation 4 (XOR-swizzled LDS rows, block map sigma) or 1 (linear LDS: blocks 16
 // samples apart already hit distinct banks; identity block map).
-template <int NCH, bool U8 = false, int D = 4>
+template <int NCH, bool U8 = false, int D = 4, int CS = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
-    using G = GeoH<NCH, D>;
+    using G = GeoH<NCH, D, CS>;
     constexpr int H = G::H, HR = G::HR, PLB = G::PLB, WINB = G::WINB, NH = G::NH, NG = G::NG;
     constexpr int TI = G::TI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -259,151 +266,193 @@ void fir_mxh_kernel(MxhParams p) {
     const int wb0 = D == 4 ? base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7)
                            : base + 4 * lane;
 
-    for (long u = wave; u < p.units; u += nwaves) {
-      const long ch = u / p.spc;
-      const long tu = (u - ch * p.spc) * p.seg_tiles;
-      const long nt = std::min(p.seg_tiles, p.tpc - tu);
-      if (nt <= 0) continue;
-      {
-        const long t0 = tu;
-        const float2* __restrict__ in = p.in + ch * p.ld_in;
-        const unsigned* __restrict__ in4 = p.in_u8 + ch * (p.ld_in / 2);  // U8: dword = 2 samples
-        const unsigned short* __restrict__ in2 =
-            reinterpret_cast<const unsigned short*>(p.in_u8) + ch * p.ld_in;
-        const float2* __restrict__ hist = p.hist + ch * (long)(K - 1);
-        float2* __restrict__ out = p.out + ch * p.ld_out;
-        const long n_in = p.n_in;
-        const long N0 = (long)TI * t0;
-        long ntf = (n_in - N0) / TI;
-        ntf = n_in < N0 ? 0 : (ntf > nt ? nt : ntf);
-        auto fetch = [&](long j) -> Raw {
-            if constexpr (U8) return fetch_pair_u8(in2, hist, j, n_in, K);
-            else return fetch_pair(in, hist, j, n_in, K);
-        };
-        auto put = [&](int a, const Raw& w, float sc) {
-            if constexpr (U8) put_pair_u8<PLB>(smem, a, w);
-            else put_pair<PLB>(smem, a, w, sc);
-        };
+    // ---- the wave's tile stream ----
+    // Units (runs of seg_tiles tiles of one channel) are dealt to waves either in per-
+    // workgroup contiguous ranges (p.blocked: wave w of the workgroup takes units w, w+8, ...,
+    // so a CU's eight waves stream eight ADJACENT runs -- one HBM locality window per CU) or
+    // grid-strided.  The wave walks its units as ONE stream of tiles: three cursors (tile k
+    // computed and stored, k+1 staged, k+2 loading) advance together, so the raw-tile
+    // prefetch crosses run boundaries; a run's first window re-reads the H samples before it
+    // (issued one tile ahead, into the history registers).
+    struct Cur {
+        long u, t, ch, tu, nt;
+        bool ok;
+    };
+    const long ust = p.blocked ? (long)kWaves : nwaves;
+    const long ub1 = p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units;
+    auto seek = [&](Cur& c, long u) {
+        c.u = u;
+        c.t = 0;
+        c.ok = u < ub1;
+        c.ch = c.ok ? u / p.spc : 0;
+        c.tu = (u - c.ch * p.spc) * p.seg_tiles;
+        c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        if (c.ok && c.nt <= 0) c.ok = false;  // (units past a channel's last tile: none by construction)
+    };
+    auto adv = [&](Cur& c) {
+        if (!c.ok) return;
+        if (++c.t >= c.nt) seek(c, c.u + ust);
+    };
+    const long n_in = p.n_in;
+    auto tile_j0 = [&](const Cur& c) { return (long)TI * (c.tu + c.t); };
+    auto tile_fast = [&](const Cur& c) { return (long)TI * (c.tu + c.t + 1) <= n_in; };
+    auto fetch = [&](const Cur& c, long j) -> Raw {
+        const float2* hist = p.hist + c.ch * (long)(K - 1);
+        if constexpr (U8)
+            return fetch_pair_u8(reinterpret_cast<const unsigned short*>(p.in_u8) + c.ch * p.ld_in, hist, j,
+                                 n_in, K);
+        else
+            return fetch_pair(p.in + c.ch * p.ld_in, hist, j, n_in, K);
+    };
+    auto put = [&](int a, const Raw& w, float sc) {
+        if constexpr (U8) put_pair_u8<PLB>(smem, a, w);
+        else put_pair<PLB>(smem, a, w, sc);
+    };
+    // 16 B (c64 pair) or 4 B (u8 pair) per lane; j = first sample of the pair
+    auto ldx = [&](const Cur& c, long j, auto nt_c) -> Raw {
+        constexpr bool NT = decltype(nt_c)::value;
+        if constexpr (U8) {
+            const unsigned* q = p.in_u8 + c.ch * (p.ld_in / 2) + (j >> 1);
+            return NT ? __builtin_nontemporal_load(q) : *q;
+        } else {
+            const f32x4* q = reinterpret_cast<const f32x4*>(p.in + c.ch * p.ld_in + j);
+            const f32x4 r = NT ? __builtin_nontemporal_load(q) : *q;
+            return make_float4(r[0], r[1], r[2], r[3]);
+        }
+    };
+    auto load_tile = [&](Raw (&dst)[NG], const Cur& c) {
+        const long j0 = tile_j0(c);
+        if (tile_fast(c)) {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) dst[k] = ldx(c, j0 + 128 * k + 2 * lane, std::true_type());
+        } else {
+            // stream start / end only: keep this path out of the hot loop (the clamped,
+            // always-dereferenceable loads would otherwise be speculated into every tile)
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < NG; ++k) dst[k] = fetch(c, j0 + 128 * k + 2 * lane);
+        }
+    };
+    // the H samples before tile c (plain loads: the neighbouring wave streams them too)
+    auto load_hist = [&](Raw (&dst)[NH], const Cur& c) {
+        const long j = tile_j0(c) - H;
+        if (j >= 0 && j + H <= n_in) {
+#pragma unroll
+            for (int k = 0; k < NH; ++k) dst[k] = ldx(c, j + 128 * k + 2 * lane, std::false_type());
+        } else {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < NH; ++k) dst[k] = fetch(c, j + 128 * k + 2 * lane);
+        }
+    };
+    auto window_scale = [&](const Raw (&nx)[NG], const Raw (&hr)[NH]) -> int {
+        if constexpr (U8) {
+            return 7;  // x128: the u8 codes minus 128, exact
+        } else {
+            float m = 0.f;
+#pragma unroll
+            for (int k = 0; k < NG; ++k) m = absmax4(m, nx[k]);
+#pragma unroll
+            for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
+            return wave_scale(m);
+        }
+    };
+    // byte offset of the sample pair (2 lane, 2 lane + 1) of history group k / new group k
+    auto hist_addr = [&](int k) {
+        if constexpr (D == 4) return (wb0 ^ (16 * (k & 7))) + 256 * k;
+        else return wb0 + 256 * k;
+    };
+    auto new_addr = [&](int k) {
+        if constexpr (D == 4) return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
+        else return wb0 + 2 * H + 256 * k;
+    };
+    // next history = the last NH groups of (history ++ this tile's groups)
+    auto roll_hist = [&](Raw (&hr)[NH], const Raw (&tile)[NG]) {
+        Raw nh[NH];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) nh[i] = NG + i < NH ? hr[(NG + i) % NH] : tile[(NG + i - NH) % NG];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) hr[i] = nh[i];
+    };
 
-        // 16 B (c64 pair) or 4 B (u8 pair) per lane; j = first sample of the pair
-        auto ldx = [&](long j) -> Raw {
-            if constexpr (U8) {
-                return __builtin_nontemporal_load(in4 + (j >> 1));
-            } else {
-                const f32x4 r = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in + j));
-                return make_float4(r[0], r[1], r[2], r[3]);
-            }
-        };
-        auto load_tile = [&](Raw (&dst)[NG], long t) {
-            const long j0 = N0 + (long)TI * t;
-            if (t < ntf) {
-#pragma unroll
-                for (int k = 0; k < NG; ++k) dst[k] = ldx(j0 + 128 * k + 2 * lane);
-            } else {
-                // stream start / end only: keep this path out of the hot loop (the clamped,
-                // always-dereferenceable loads would otherwise be speculated into every tile)
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int k = 0; k < NG; ++k) dst[k] = fetch(j0 + 128 * k + 2 * lane);
-            }
-        };
-        auto window_scale = [&](const Raw (&nx)[NG], const Raw (&hr)[NH]) -> int {
-            if constexpr (U8) {
-                return 7;  // x128: the u8 codes minus 128, exact
-            } else {
-                float m = 0.f;
-#pragma unroll
-                for (int k = 0; k < NG; ++k) m = absmax4(m, nx[k]);
-#pragma unroll
-                for (int k = 0; k < NH; ++k) m = absmax4(m, hr[k]);
-                return wave_scale(m);
-            }
-        };
-        // byte offset of the sample pair (2 lane, 2 lane + 1) of history group k / new group k
-        auto hist_addr = [&](int k) {
-            if constexpr (D == 4) return (wb0 ^ (16 * (k & 7))) + 256 * k;
-            else return wb0 + 256 * k;
-        };
-        auto new_addr = [&](int k) {
-            if constexpr (D == 4) return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
-            else return wb0 + 2 * H + 256 * k;
-        };
-        // next history = the last NH groups of (history ++ this tile's groups)
-        auto roll_hist = [&](Raw (&hr)[NH], const Raw (&tile)[NG]) {
-            Raw nh[NH];
-#pragma unroll
-            for (int i = 0; i < NH; ++i) nh[i] = NG + i < NH ? hr[(NG + i) % NH] : tile[(NG + i - NH) % NG];
-#pragma unroll
-            for (int i = 0; i < NH; ++i) hr[i] = nh[i];
-        };
-
-        // PD raw tiles in flight per wave (8 groups' worth of registers: 1 tile at D = 4,
-        // 4 at D = 1, whose tiles are 4x shorter); rr[t % PD] holds tile t until staged
-        constexpr int PD = 8 / NG;
-        Raw rr[PD][NG], hr[NH];
-#pragma unroll
-        for (int k = 0; k < NH; ++k) hr[k] = fetch(N0 - H + 128 * k + 2 * lane);
-        load_tile(rr[0], 0);
-#pragma unroll
-        for (int q = 1; q < PD; ++q)
-            if (q < nt) load_tile(rr[q], q);
-        int s_cur = window_scale(rr[0], hr);
+    // one raw tile in flight per wave (NG <= 8 groups of registers)
+    static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
+    Cur cm, st, ld;
+    seek(cm, p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave);
+    if (cm.ok) {
+        Raw nx[NG], hr[NH];
+        load_hist(hr, cm);
+        load_tile(nx, cm);
+        int s_cur = window_scale(nx, hr);
         {
             const float sc = exp2i(s_cur);
 #pragma unroll
             for (int k = 0; k < NH; ++k) put(hist_addr(k), hr[k], sc);
 #pragma unroll
-            for (int k = 0; k < NG; ++k) put(new_addr(k), rr[0][k], sc);
-            roll_hist(hr, rr[0]);
+            for (int k = 0; k < NG; ++k) put(new_addr(k), nx[k], sc);
         }
-        if (PD < nt) load_tile(rr[0], PD);
+        st = cm;
+        adv(st);
+        if (st.ok && st.t == 0) load_hist(hr, st);
+        else roll_hist(hr, nx);
+        if (st.ok) load_tile(nx, st);
+        ld = st;
+        adv(ld);
 
-        auto body = [&](auto tau_c, long t, Raw (&nx)[NG]) {
+        auto body = [&](auto tau_c) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
-            const long tp = t + 1 + PD;  // the tile whose loads replace nx's
-            const bool fast2 = tp < ntf;
-            // prefetch source: tile tp, or the zeroed dummy buffer (scalar select)
-            const long j2 = N0 + (long)TI * tp;
-            const float2* src2 = fast2 ? in + j2 : p.dummy;
-            const unsigned* src2u =
-                fast2 ? in4 + (j2 >> 1) : reinterpret_cast<const unsigned*>(p.dummy);
+            const bool fast2 = ld.ok && tile_fast(ld);
+            const bool ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
+            // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
+            const long j2 = tile_j0(ld);
+            const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;
+            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch * (p.ld_in / 2) + (j2 >> 1)
+                                          : reinterpret_cast<const unsigned*>(p.dummy);
             const int s_next = window_scale(nx, hr);
             const float scn = exp2i(s_next);
             constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
             Raw keep[NK];
-            f32x4 cr = {0.f, 0.f, 0.f, 0.f}, ci = {0.f, 0.f, 0.f, 0.f};
+            f32x4 cr[CS], ci[CS];
+#pragma unroll
+            for (int j = 0; j < CS; ++j) {
+                cr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
             u32x4 fb[2][4];
-            auto read_frags = [&](u32x4 (&f)[4], int c) {
-                const int a = rb[c] + TAU * WINB;
+            // column set j of the tile reads 256 samples (D = 1) further into the window
+            auto read_frags = [&](u32x4 (&f)[4], int c, int j) {
+                const int a = rb[c] + TAU * WINB + j * 2 * 256 * D;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (!U8 || (q & 1) == 0)
                         f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
             };
-            read_frags(fb[0], 0);
+            read_frags(fb[0], 0, 0);
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
+            for (int i = 0; i < CS * NCH; ++i) {
+                const int j = i / NCH, c = i % NCH;
                 {
-                    if (c + 1 < NCH) read_frags(fb[(c + 1) & 1], c + 1);
+                    if (i + 1 < CS * NCH) read_frags(fb[(i + 1) & 1], (i + 1) % NCH, (i + 1) / NCH);
                     __builtin_amdgcn_sched_barrier(0);
-                    const u32x4(&f)[4] = fb[c & 1];
-                    cr = mfma(al[c], f[0], cr);
-                    ci = mfma(al[c], f[2], ci);
+                    const u32x4(&f)[4] = fb[i & 1];
+                    cr[j] = mfma(al[c], f[0], cr[j]);
+                    ci[j] = mfma(al[c], f[2], ci[j]);
                     if (!U8) {
-                        cr = mfma(ah[c], f[1], cr);
-                        ci = mfma(ah[c], f[3], ci);
+                        cr[j] = mfma(ah[c], f[1], cr[j]);
+                        ci[j] = mfma(ah[c], f[3], ci[j]);
                     }
-                    cr = mfma(ah[c], f[0], cr);
-                    ci = mfma(ah[c], f[2], ci);
+                    cr[j] = mfma(ah[c], f[0], cr[j]);
+                    ci[j] = mfma(ah[c], f[2], ci[j]);
                 }
-                if (c == 0) {  // next window's history = this tile's tail (old hr)
+                if (i == 0) {  // window k+1's history (old hr); then tile k+2's, if it opens a run
 #pragma unroll
                     for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
+                    if (ld_run) load_hist(hr, ld);
                 }
 #pragma unroll
                 for (int k = 0; k < NG; ++k) {
-                    if ((k < NCH - 1 ? k : NCH - 1) != c) continue;
+                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) != i) continue;
                     put(WN + new_addr(k), nx[k], scn);
                     if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
                     if constexpr (U8) {
@@ -415,47 +464,48 @@ void fir_mxh_kernel(MxhParams p) {
                     }
                 }
             }
-            {   // history of tile t+2's window: roll in the staged tile's tail
+            if (!ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
                 Raw tile[NG];
 #pragma unroll
                 for (int k = 0; k < NG; ++k) tile[k] = keep[k < (NG > NH ? NG - NH : 0) ? 0 : k - (NG > NH ? NG - NH : 0)];
                 roll_hist(hr, tile);
             }
-            if (!fast2 && tp < nt) load_tile(nx, tp);
+            if (!fast2 && ld.ok) load_tile(nx, ld);
             const int so = -(s_cur + p.sh);
-            const long m = (t0 + t) * kTileOut + 16 * sv + 4 * g;  // sv = block of column v
-            float yr[4], yi[4];
+            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
+            const long m0 = (cm.tu + cm.t) * G::TO;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                yr[i] = __builtin_amdgcn_ldexpf(cr[i], so);
-                yi[i] = __builtin_amdgcn_ldexpf(ci[i], so);
-            }
-            if (p.vec_out && (t0 + t + 1) * kTileOut <= p.n_out) {
-                f32x4* o4 = reinterpret_cast<f32x4*>(out + m);
-                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                __builtin_nontemporal_store(y0, o4);
-                __builtin_nontemporal_store(y1, o4 + 1);
-            } else {
+            for (int j = 0; j < CS; ++j) {
+                const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
+                float yr[4], yi[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+                for (int i = 0; i < 4; ++i) {
+                    yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
+                    yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
+                }
+                if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
+                    f32x4* o4 = reinterpret_cast<f32x4*>(out + m);
+                    const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                    const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                    __builtin_nontemporal_store(y0, o4);
+                    __builtin_nontemporal_store(y1, o4 + 1);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+                }
             }
             s_cur = s_next;
+            cm = st;
+            st = ld;
+            adv(ld);
         };
-
-        // unrolled over lcm(2, PD) tiles: ring half (t & 1) and raw slot ((t + 1) % PD) are
-        // compile-time in every body
-        constexpr int U = PD > 2 ? PD : 2;
-        for (long t = 0; t < nt; t += U) {
-            [&]<int... I>(std::integer_sequence<int, I...>) {
-                bool go = true;
-                ((go = go && (t + I < nt),
-                  go ? (body(std::integral_constant<int, I & 1>(), t + I, rr[(I + 1) % PD]), 0) : 0),
-                 ...);
-            }(std::make_integer_sequence<int, U>());
+        // two tiles per iteration: the window ring half is compile-time in every body
+        while (cm.ok) {
+            body(std::integral_constant<int, 0>());
+            if (!cm.ok) break;
+            body(std::integral_constant<int, 1>());
         }
-      }
     }
 
     if (p.hist_next) {  // stream history carry, spread over the whole grid
@@ -537,27 +587,34 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    p.tpc = ceil_div(std::max(0L, fp.n_out), kTileOut);
+    const int cs = D == 1 ? kCs1 : 1;
+    p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     const long W = (long)kWaves * cus;
+    // D = 4: runs of kRunTiles tiles dealt in per-CU blocks (0.516-0.525 vs 0.556-0.559 ms with
+    // one long range per wave at configs[1]; profiles/r02_fir_runs.txt).  D = 1 banks keep
+    // whole-channel units grid-strided (no gain from runs there).
+    const int run = D == 4 ? kRunTiles : 0;
     long spc = nch >= W ? 1 : ceil_div(W, nch);
     spc = std::max(1L, std::min(spc, p.tpc));
     p.seg_tiles = std::max(1L, ceil_div(p.tpc, spc));
+    if (run > 0) p.seg_tiles = std::max(1L, std::min<long>(run, p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
+    p.blocked = run > 0;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
-#define SDRGPU_MXH_GO(CC, U, DD)                                                               \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD>), dim3(blocks), dim3(kBlock),                \
-                       (size_t)kWaves * (GeoH<CC, DD>::WAVE), s, p)
+#define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
+                       (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
-        if (u8) SDRGPU_MXH_GO(CC, true, 4);                                                    \
-        else SDRGPU_MXH_GO(CC, false, 4);                                                      \
+        if (u8) SDRGPU_MXH_GO(CC, true, 4, 1);                                                 \
+        else SDRGPU_MXH_GO(CC, false, 4, 1);                                                   \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
 #define SDRGPU_MXH_CASE1(CC)                                                                   \
     if (D == 1 && NCH == CC) {                                                                 \
-        SDRGPU_MXH_GO(CC, false, 1);                                                           \
+        SDRGPU_MXH_GO(CC, false, 1, kCs1);                                                     \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
