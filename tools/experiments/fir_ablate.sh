@@ -1,0 +1,47 @@
+#!/bin/bash
+# Build ablated copies of the headline FIR kernel into tools/experiments/abl/ (never into the
+# product library): nomfma = MFMAs replaced by one VALU add per fragment (LDS reads kept),
+# noload = every fast-path tile load reads the 8 KiB dummy buffer (compute + stores only).
+# Run one with: python tools/experiments/run_with_lib.py tools/experiments/abl/lib_<v>.so bench.py ...
+set -e
+cd "$(dirname "$0")/../.."
+mkdir -p tools/experiments/abl
+make -C unnamed-rust-sdr_amd -s
+OBJS=$(ls unnamed-rust-sdr_amd/build/*.o | grep -v fir_mxh.o)
+for v in ${VARIANTS:-nomfma noload}; do
+  src=tools/experiments/abl/fir_mxh_$v.hip
+  cp unnamed-rust-sdr_amd/csrc/fir_mxh.hip $src
+  if [ $v = nomfma ]; then
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);"""
+assert old in s
+s = s.replace(old, """    c[0] += __uint_as_float(b[0] & 0x3ffu);
+    return c;""")
+open(p, 'w').write(s)
+PY
+  elif [ $v = noload ]; then
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;"
+assert old in s
+s = s.replace(old, "const float2* src2 = p.dummy;")
+open(p, 'w').write(s)
+PY
+  elif [ $v = wvdiv ]; then  # wave index left divergent (VGPR cursor math, no SGPR spills)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);"
+assert old in s
+s = s.replace(old, "const int wv = threadIdx.x >> 6;")
+open(p, 'w').write(s)
+PY
+  fi
+  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+done
+echo built

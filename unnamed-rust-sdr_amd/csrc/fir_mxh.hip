@@ -175,8 +175,9 @@ __device__ __forceinline__ void put_pair(char* lds, int a, const float4& f, floa
     st32(lds, a + 3 * PLB, l);
 }
 
+// a left-leaning chain folds into two v_max3_f32 with |.| source modifiers
 __device__ __forceinline__ float absmax4(float m, const float4& f) {
-    return fmaxf(fmaxf(m, fmaxf(fabsf(f.x), fabsf(f.y))), fmaxf(fabsf(f.z), fabsf(f.w)));
+    return fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(f.x)), fabsf(f.y)), fabsf(f.z)), fabsf(f.w));
 }
 
 // window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float.  The
@@ -218,7 +219,8 @@ void fir_mxh_kernel(MxhParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    // wave-uniform (readfirstlane), so the tile cursors and channel addressing stay scalar
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long wave = (long)blockIdx.x * kWaves + wv;
     const long nwaves = (long)gridDim.x * kWaves;
     const int g = lane >> 4, v = lane & 15;
