@@ -284,6 +284,33 @@ def test_fir_full_size_c2_properties(sdr, oracle):
         assert np.array_equal(y2, 2 * y1)
 
 
+def test_fir_mx_run_boundaries_whole_stream(sdr, oracle):
+    """The D = 4 kernel deals runs of 8 tiles to each CU's waves and walks a wave's runs as
+    one pipeline (a run's first window re-reads the 256 samples before it).  At 2^25 + a
+    ragged tail every wave owns two or more runs, so run starts, the cross-run prefetch and
+    the partial last tile all occur; the WHOLE output is compared with the oracle, in two
+    device blocks whose cut is not tile-aligned."""
+    from sdrgpu.device import DeviceBuffer
+    import scipy.signal as ss
+    n = (1 << 25) + 4 * 777 + 3
+    K, D = 255, 4
+    taps = ss.firwin(K, 0.2).astype(np.float32)
+    rng = np.random.default_rng(77)
+    x = ((rng.standard_normal(n, dtype=np.float32) + 1j * rng.standard_normal(n, dtype=np.float32))
+         * np.float32(0.3)).astype(np.complex64)
+    dx = DeviceBuffer.from_numpy(x)
+    n_out = n // D
+    dy = DeviceBuffer.empty(n_out + 8, np.complex64)
+    f = fir(sdr, taps, 1, D)
+    cut = 4 * 1234567 + 2
+    m1 = f.process_dev(dx.ptr, cut, dy.ptr, n_out + 8)
+    m2 = f.process_dev(dx.ptr + 8 * cut, n - cut, dy.ptr + 8 * m1, n_out + 8 - m1)
+    f.sync()
+    assert m1 + m2 == n_out
+    ref = oracle.fir_batch(taps, x[None, :], D, nthreads=16)[0]
+    assert_parity(dy.download(n_out), ref, what="2^25 stream, two blocks")
+
+
 @pytest.mark.parametrize("algo", ["direct", "mx", "auto"])
 def test_time_shard_halo_equivalence(sdr, oracle, algo):
     """Multi-GPU time sharding (bench.py): a shard primed with the 256 preceding samples

@@ -1,14 +1,23 @@
 """Run a script (bench.py, bench_configs.py) against another build of the library, e.g. an
-ablation from fir_ablate.sh: python tools/experiments/run_with_lib.py LIB.so SCRIPT [args]."""
+ablation from fir_ablate.sh: python tools/experiments/run_with_lib.py LIB.so SCRIPT [args].
+The package loads its library at import, so sdrgpu._lib is pre-seeded in sys.modules with
+LIB_PATH pointing at LIB.so before the package itself is imported."""
+import importlib.util
 import os
 import runpy
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(ROOT, "unnamed-rust-sdr_amd"))
+PKG = os.path.join(ROOT, "unnamed-rust-sdr_amd")
+sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
-import sdrgpu._lib as L  # noqa: E402
-
-L.LIB_PATH = os.path.abspath(sys.argv[1])
+spec = importlib.util.spec_from_file_location("sdrgpu._lib", os.path.join(PKG, "sdrgpu", "_lib.py"))
+mod = importlib.util.module_from_spec(spec)
+sys.modules["sdrgpu._lib"] = mod
+spec.loader.exec_module(mod)
+mod.LIB_PATH = os.path.abspath(sys.argv[1])
+import sdrgpu  # noqa: E402,F401  (package init now loads LIB.so)
+assert sdrgpu._lib.lib()._name == mod.LIB_PATH, "variant library not loaded"
+print(f"[run_with_lib] {mod.LIB_PATH}", file=sys.stderr)
 sys.argv = sys.argv[2:]
 runpy.run_path(sys.argv[0], run_name="__main__")
