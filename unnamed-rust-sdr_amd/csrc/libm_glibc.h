@@ -308,6 +308,27 @@ SDR_LIBM_FN void sdr_sincosf_bf(float y, float* sinp, float* cosp) {
     *cosp = tiny ? 1.0f : ((n & 1) ? sp : cp);
 }
 
+/* f32 division a / b, correctly rounded, for finite nonzero a, b whose quotient is a normal
+ * float -- the only operands whose quotient the branch-free atan2f/atanf below use (zeros,
+ * infinities, NaNs and |y/x| beyond 2^+-60 are replaced by the special-case selects).  On the
+ * device it is evaluated in f64: a reciprocal refined once by Newton and a corrected quotient
+ * (relative error < 2^-52), rounded once to f32.  The exact quotient of two 24-bit significands
+ * is never within 2^-49 (relative) of an f32 rounding midpoint, so that rounding equals
+ * IEEE a / b; checked bit-exact against the compiler's a / b on 2^36 GPU pairs
+ * (tools/fdiv_check.hip).  Seven dependent f64 ops instead of the ten-deep v_div_scale /
+ * v_rcp / fma / v_div_fmas / v_div_fixup chain with its VCC hazards. */
+SDR_LIBM_FN float sdr_fdiv(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double bd = (double)b, ad = (double)a;
+    const double r0 = __builtin_amdgcn_rcp(bd);
+    const double r1 = fma(r0, fma(-bd, r0, 1.0), r0);
+    const double q0 = ad * r1;
+    return (float)fma(fma(-bd, q0, ad), r1, q0);
+#else
+    return a / b;
+#endif
+}
+
 SDR_LIBM_FN float sdr_atanf_bf(float x) {
     /* finite x (sdr_atan2f_bf routes NaN through the reference function) */
     const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
@@ -331,7 +352,7 @@ SDR_LIBM_FN float sdr_atanf_bf(float x) {
     const float num2 = ax - (float)1.5, den2 = one + (float)1.5 * ax;
     const float num = c0 ? num0 : c1 ? num1 : c2 ? num2 : -(float)1.0;
     const float den = c0 ? den0 : c1 ? den1 : c2 ? den2 : ax;
-    const float q = num / den;
+    const float q = sdr_fdiv(num, den);
     const float xr = small ? x : q;
     const float z = xr * xr;
     const float w = z * z;
@@ -386,7 +407,7 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     const int32_t k = (iy - ix) >> 23;
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
     /* common path (its value is discarded wherever a special case applies) */
-    const float qq = y / x;
+    const float qq = sdr_fdiv(y, x);
     const float za = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
     const float z = k > 60 ? pi_o_2 + (float)0.5 * pi_lo : ((hx < 0) & (k < -60)) ? 0.0f : za;
     const float t = z - pi_lo;
