@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--c5-log2n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="c5 only: run as this many ranks (self-launched, one process per GPU)")
     return ap.parse_args()
 
 
@@ -331,7 +333,8 @@ def bench_c5(args):
     from sdrgpu.shard import Comm, channel_range, unique_id
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ranks beyond the visible GPUs share them round-robin (a rehearsal on a 1-GPU box)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, sdrgpu.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -367,7 +370,9 @@ def bench_c5(args):
     ck = nch // 2
     res["spot_check_max_over_rms"] = spot_check(pyoracle, taps, x, y, ck, n)
     assert res["spot_check_max_over_rms"] <= 1e-5, res["spot_check_max_over_rms"]
-    if dist is not None:
+    if dist is not None and world > sdrgpu.device_count():
+        res["rccl"] = "skipped: ranks share a GPU (RCCL needs one device per rank)"
+    elif dist is not None:
         # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately);
         # uneven channel blocks (nch % world != 0) go through grouped send / recv
         ids = [unique_id() if rank == 0 else None]
@@ -438,6 +443,11 @@ def bench_src(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.config != "c5":
+            sys.exit("--gpus > 1 applies to --config c5 only")
+        from bench import launch_ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
     todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src"] if args.config == "all" else [args.config]
     for c in todo:
         r = {"c1": bench_c1, "c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
