@@ -40,7 +40,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "all"])
+    ap.add_argument("--config", default="all", choices=["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -169,6 +169,49 @@ def bench_c3(args):
                                "cores": 1, "kind": "proxy",
                                "sample": f"{done} NumPy pocketfft 64k frames (proxy for rustfft 3.0), {el:.1f} s"}
     return res
+
+
+# ------------------------------------------------------------------------------ ex
+def bench_ex(args):
+    """The reference examples' FFT shapes at throughput scale (not BASELINE configs): the
+    live spectrum of examples/live.rs (1000-point frames of rtl_tcp-rate IQ, shown in dB by
+    ComplexSeries::plot) as an STFT with hop 500 and the fused dB output, and the
+    14,400-point rfft of examples/fft.rs (take(0.1) at 144 kHz) batched over 4096 frames --
+    both through the any-N (mixed-radix 2/3/5) kernels."""
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, synchronize
+    out = []
+    n = 1 << 26
+    st = sdrgpu.fft.Stft(1000, 500, output="db")
+    x = DeviceBuffer.empty(n)
+    fill(x, n, 21)
+    nf = st.output_len(n)
+    y = DeviceBuffer.empty(nf * 1000 // 2 + 1)  # f32 dB values: half the c64 bytes
+
+    def step():
+        st.reset()
+        assert st.process_dev(x.ptr, n, y.ptr, nf) == nf
+
+    wall, ms = time_events(step, st.stream(), args.steps, args.warmup, lambda: (st.sync(), synchronize()))
+    out.append({"config": "ex_live: examples/live.rs spectrum shape -- 1000-point STFT, hop 500, "
+                          "fused 20*log10|X| (f32) output, 2^26 c64 samples",
+                "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
+                "frames": nf, "roofline": roof(8 + 2 * 4, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)})
+    N, count = 14400, 4096
+    p = sdrgpu.fft.FftPlan(N)
+    xr = DeviceBuffer.empty(N * count // 2)  # f32 frames (c64-sized buffer units)
+    fill(xr, N * count // 2, 22)
+    yr = DeviceBuffer.empty((N - N // 2) * count)
+
+    def step2():
+        p.exec_real_dev(xr.ptr, yr.ptr, count)
+
+    wall, ms = time_events(step2, p.stream(), args.steps, args.warmup, lambda: (p.sync(), synchronize()))
+    out.append({"config": "ex_rfft: examples/fft.rs rfft shape -- 14400-point rfft (f32 in, 7200 "
+                          "c64 bins out) x 4096 frames",
+                "metric": "real Msamples/s (input)", "value": round(N * count / (ms * 1e-3) / 1e6, 1),
+                "roofline": roof(4 + 4, N * count, ms), "wall_ms_per_step": round(wall * 1e3, 3)})
+    return out
 
 
 # ------------------------------------------------------------------------------ c2u8
@@ -448,12 +491,13 @@ def main():
             sys.exit("--gpus > 1 applies to --config c5 only")
         from bench import launch_ranks
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
-    todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src"] if args.config == "all" else [args.config]
+    todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex"] if args.config == "all" else [args.config]
     for c in todo:
         r = {"c1": bench_c1, "c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
-             "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src}[c](args)
-        if r is not None:
-            print(json.dumps(r), flush=True)
+             "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src, "ex": bench_ex}[c](args)
+        for line in (r if isinstance(r, list) else [r]):
+            if line is not None:
+                print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -191,6 +191,9 @@ int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t cou
 /* rfft: `count` frames of n F32 samples -> count frames of n - n/2 C64 values: the collated
  * output with its first n/2 entries drained (fft.rs:35), i.e. X[0 .. n - n/2) * 1/sqrt(n). */
 int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count);
+/* rfft on device pointers (count frames of n F32 in, n - n/2 outputs each out), enqueued
+ * on the plan's stream. */
+int sdrgpu_rfft_exec_dev(sdrgpu_fft* h, const float* d_in, void* d_out, size_t count);
 /* Output format of exec / rfft_exec (and the STFT): SDRGPU_FFT_OUT_COMPLEX (default, C64) or
  * SDRGPU_FFT_OUT_DB -- one f32 per bin, 20*log10(|X * 1/sqrt(n)|): the magnitude-in-dB
  * conversion every spectrum plot of the reference applies to fft's output

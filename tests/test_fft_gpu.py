@@ -86,6 +86,22 @@ def test_fft_any_golden(sdr):
     assert_parity(y, g["sy"], what="golden stft 1000")
 
 
+def test_rfft_device_pointers_match_host_path(sdr):
+    """sdrgpu_rfft_exec_dev (device-resident frames, the examples/fft.rs batch shape) gives
+    exactly the host-pointer rfft's values."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(5)
+    for n, count in ((14400, 7), (1000, 33), (4096, 3)):
+        x = rng.standard_normal((count, n)).astype(np.float32)
+        p = sdr.fft.FftPlan(n)
+        ref = p.exec_real(x)
+        dx = DeviceBuffer.from_numpy(x)
+        dy = DeviceBuffer.empty(count * (n - n // 2), np.complex64)
+        p.exec_real_dev(dx.ptr, dy.ptr, count)
+        p.sync()
+        assert np.array_equal(dy.download().reshape(count, n - n // 2), ref)
+
+
 @pytest.mark.parametrize("n", [1000, 1001, 14400, 4099, 65536])
 def test_rfft_any_size(sdr, oracle, n):
     rng = np.random.default_rng(n)

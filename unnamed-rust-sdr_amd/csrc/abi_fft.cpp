@@ -132,6 +132,19 @@ int sdrgpu_fft_exec(sdrgpu_fft* h, const void* in, void* out, size_t count) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_rfft_exec_dev(sdrgpu_fft* h, const float* d_in, void* d_out, size_t count) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    if (count == 0) return SDRGPU_OK;
+    if (!d_in || !d_out) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    FftFrames fr{};
+    fr.mode = 2;
+    fr.in_real = d_in;
+    fr.nframes = (long)count;
+    return h->run(fr, static_cast<float2*>(d_out), 1);
+}
+
 int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count) {
     if (!h) return SDRGPU_ERR_INVALID;
     if (count == 0) return SDRGPU_OK;
@@ -143,11 +156,8 @@ int sdrgpu_rfft_exec(sdrgpu_fft* h, const float* in, void* out, size_t count) {
     int st;
     if ((st = h->stage_in.ensure(in_bytes)) || (st = h->stage_out.ensure(out_bytes))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(h->stage_in.ptr, in, in_bytes, hipMemcpyHostToDevice, h->stream.cur));
-    FftFrames fr{};
-    fr.mode = 2;
-    fr.in_real = static_cast<const float*>(h->stage_in.ptr);
-    fr.nframes = (long)count;
-    if ((st = h->run(fr, static_cast<float2*>(h->stage_out.ptr), 1))) return st;
+    if ((st = sdrgpu_rfft_exec_dev(h, static_cast<const float*>(h->stage_in.ptr), h->stage_out.ptr, count)))
+        return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(out, h->stage_out.ptr, out_bytes, hipMemcpyDeviceToHost, h->stream.cur));
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
     return SDRGPU_OK;

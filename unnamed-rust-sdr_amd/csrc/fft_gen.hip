@@ -8,9 +8,10 @@
 //
 // Three plans, chosen on the host from N's factorisation:
 //   * mixed-radix tile (N <= 4096, every prime factor <= 13): B = 4096/N transforms per
-//     256-lane workgroup in a ping-pong pair of LDS buffers (64 KiB), one Stockham autosort
+//     256-lane workgroup in one 32 KiB LDS buffer, one in-place Stockham autosort
 //     pass per radix (16/8/4/2, 3, 5, and a generic odd-radix pair kernel for 7/11/13);
-//     twiddles are loads from a W_N table computed in f64 on the host (no recurrence error);
+//     twiddles: one load per butterfly from a W_N table computed in f64 on the host, its
+//     powers by a log-depth product tree; index arithmetic by plan-time magic multipliers;
 //     the STFT frame gather and the collated store are folded into the first / last pass.
 //   * mixed-radix four-step (N > 4096 smooth, N = N1 * N2 with both <= 4096):
 //     pass A = N2-point FFTs down the columns n1 of x[n1 + N1 n2] (rows of C contiguous
@@ -43,9 +44,26 @@ constexpr int kGenBlock = 256;
 constexpr int kGenTile = 4096;   // complex points per LDS buffer
 constexpr int kMaxPass = 16;
 
+// division by a plan-time constant d < 2^16 for dividends < 2^16: q = umulhi(n, ceil(2^32/d))
+// (exact while n d < 2^32), one v_mul_hi_u32 instead of a ~30-instruction integer division
+struct FastDiv {
+    unsigned m = 0;
+    int d = 1;
+    __host__ void set(int dv) {
+        d = dv;
+        m = dv > 1 ? (unsigned)((0x100000000ULL + (unsigned long long)dv - 1) / (unsigned long long)dv) : 0u;
+    }
+    __device__ __forceinline__ int div(int n) const {
+        return d == 1 ? n : (int)__umulhi((unsigned)n, m);
+    }
+};
+
 struct RadixList {
     int n = 0;
     int R[kMaxPass] = {};
+    FastDiv dq[kMaxPass];   // pass p: N / R[p] (butterflies per transform)
+    FastDiv dns[kMaxPass];  // pass p: Ns = product of the earlier radices
+    FastDiv dn;             // N
 };
 
 // ---- butterflies -----------------------------------------------------------------------
@@ -130,60 +148,70 @@ __device__ __forceinline__ void dft_any(float2* v, const float2* __restrict__ tw
     else dft_odd<R>(v, tw, N);
 }
 
-// One Stockham autosort pass over B transforms of size N (transform f at f * N): butterfly
-// (f, j), j < N/R, k = j mod Ns, reads src[f N + j + r N/R], twiddles by W_N^{r k N/(Ns R)}
-// (r k N/(Ns R) < N: a plain table index), writes dst[f N + (j - k) R + k + r Ns].
+// One Stockham autosort pass over B transforms of size N (transform f at f * N), in place:
+// every lane first reads and transforms its butterflies (f, j), j < N/R, k = j mod Ns
+// (reads buf[f N + j + r N/R], twiddles by W_N^{r k N/(Ns R)}, a plain table index), then,
+// after a barrier, writes them to buf[f N + (j - k) R + k + r Ns].  One LDS buffer instead of
+// a ping-pong pair doubles the workgroups per CU.  B N <= 4096, so a lane owns at most
+// ceil(4096 / (R 256)) butterflies.
 template <int R>
-__device__ __forceinline__ void gen_pass(const float2* __restrict__ src, float2* __restrict__ dst,
-                                         int N, int B, int Ns, const float2* __restrict__ tw) {
+__device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
+                                         const float2* __restrict__ tw, const FastDiv& dq,
+                                         const FastDiv& dns) {
+    constexpr int NB = (kGenTile / R + kGenBlock - 1) / kGenBlock;
     const int Q = N / R;
     const int total = B * Q;
     const int step = N / (Ns * R);
-    for (int g = threadIdx.x; g < total; g += kGenBlock) {
-        const int f = g / Q, j = g - f * Q;
-        const int k = j % Ns;
-        const float2* s = src + f * N + j;
-        float2 v[R];
+    float2 v[NB][R];
+    int dsto[NB];
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[r] = s[r * Q];
-        if (Ns > 1) {
+    for (int u = 0; u < NB; ++u) {
+        const int g = threadIdx.x + u * kGenBlock;
+        dsto[u] = -1;
+        if (g < total) {
+            const int f = dq.div(g), j = g - f * Q;
+            const int k = j - Ns * dns.div(j);
+            const float2* s = buf + f * N + j;
 #pragma unroll
-            for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * step]);
+            for (int r = 0; r < R; ++r) v[u][r] = s[r * Q];
+            if (Ns > 1) twiddle_tree<R>(v[u], tw[k * step]);  // W^{r k step} = (W^{k step})^r
+            dft_any<R>(v[u], tw, N);
+            dsto[u] = f * N + (j - k) * R + k;
         }
-        dft_any<R>(v, tw, N);
-        float2* d = dst + f * N + (j - k) * R + k;
+    }
+    __syncthreads();
 #pragma unroll
-        for (int r = 0; r < R; ++r) d[r * Ns] = v[r];
+    for (int u = 0; u < NB; ++u) {
+        if (dsto[u] >= 0) {
+            float2* d = buf + dsto[u];
+#pragma unroll
+            for (int r = 0; r < R; ++r) d[r * Ns] = v[u][r];
+        }
     }
 }
 
-// Runs the plan's passes over B transforms of size N held in b0; returns the buffer that
-// holds the natural-order result (b0 or b1).
-__device__ float2* gen_engine(float2* b0, float2* b1, int N, int B, const RadixList& rl,
-                              const float2* __restrict__ tw) {
-    float2* cur = b0;
-    float2* nxt = b1;
+// Runs the plan's passes in place over B transforms of size N held in buf.
+__device__ void gen_engine(float2* buf, int N, int B, const RadixList& rl,
+                           const float2* __restrict__ tw) {
     int Ns = 1;
     for (int ps = 0; ps < rl.n; ++ps) {
         const int R = rl.R[ps];
+        const FastDiv& dq = rl.dq[ps];
+        const FastDiv& dns = rl.dns[ps];
         switch (R) {
-        case 2: gen_pass<2>(cur, nxt, N, B, Ns, tw); break;
-        case 3: gen_pass<3>(cur, nxt, N, B, Ns, tw); break;
-        case 4: gen_pass<4>(cur, nxt, N, B, Ns, tw); break;
-        case 5: gen_pass<5>(cur, nxt, N, B, Ns, tw); break;
-        case 7: gen_pass<7>(cur, nxt, N, B, Ns, tw); break;
-        case 8: gen_pass<8>(cur, nxt, N, B, Ns, tw); break;
-        case 11: gen_pass<11>(cur, nxt, N, B, Ns, tw); break;
-        case 13: gen_pass<13>(cur, nxt, N, B, Ns, tw); break;
-        default: gen_pass<16>(cur, nxt, N, B, Ns, tw); break;
+        case 2: gen_pass<2>(buf, N, B, Ns, tw, dq, dns); break;
+        case 3: gen_pass<3>(buf, N, B, Ns, tw, dq, dns); break;
+        case 4: gen_pass<4>(buf, N, B, Ns, tw, dq, dns); break;
+        case 5: gen_pass<5>(buf, N, B, Ns, tw, dq, dns); break;
+        case 7: gen_pass<7>(buf, N, B, Ns, tw, dq, dns); break;
+        case 8: gen_pass<8>(buf, N, B, Ns, tw, dq, dns); break;
+        case 11: gen_pass<11>(buf, N, B, Ns, tw, dq, dns); break;
+        case 13: gen_pass<13>(buf, N, B, Ns, tw, dq, dns); break;
+        default: gen_pass<16>(buf, N, B, Ns, tw, dq, dns); break;
         }
         __syncthreads();
-        float2* t = cur;
-        cur = nxt;
-        nxt = t;
         Ns *= R;
     }
-    return cur;
 }
 
 struct GenTileArgs {
@@ -201,20 +229,20 @@ __global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
     extern __shared__ float2 glds[];
     const int N = a.N, B = a.B, L = B * N;
     float2* b0 = glds;
-    float2* b1 = glds + L;
     const long f0 = (long)blockIdx.x * B;
     const int nf = (int)min((long)B, a.nframes - f0);
     for (int p = threadIdx.x; p < L; p += kGenBlock) {
-        const int f = p / N, n = p - f * N;
+        const int f = a.rl.dn.div(p), n = p - f * N;
         b0[p] = f < nf ? frame_sample(a.src, N, f0 + f, n) : make_float2(0.f, 0.f);
     }
     __syncthreads();
-    const float2* X = gen_engine(b0, b1, N, B, a.rl, a.tw);
+    gen_engine(b0, N, B, a.rl, a.tw);
+    const float2* X = b0;
     if (a.store_mode == 0 || a.store_mode == 3) {
         // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o
         const int sh = N - N / 2;
         for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
-            const int f = p / N, o = p - f * N;
+            const int f = a.rl.dn.div(p), o = p - f * N;
             int k = o + sh;
             if (k >= N) k -= N;
             const float2 x = X[f * N + k];
@@ -223,7 +251,7 @@ __global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
         }
     } else {
         for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
-            const int f = p / N, k = p - f * N;
+            const int f = a.rl.dn.div(p), k = p - f * N;
             store_bin(a.out, f0 + f, N, k, X[p], a.store_mode, a.norm);
         }
     }
@@ -244,6 +272,15 @@ struct Gen4Args {
     float2* out;
 };
 
+// p / d for p, d <= 4096 with d varying per workgroup: f32 reciprocal estimate, then one
+// correction step each way (exact: the estimate is off by at most one)
+__device__ __forceinline__ int small_div(int p, int d) {
+    int q = (int)((float)p * __builtin_amdgcn_rcpf((float)d));
+    q += (q + 1) * d <= p;
+    q -= q * d > p;
+    return q;
+}
+
 __global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
     extern __shared__ float2 glds[];
     const int N1 = a.N1, N2 = a.N2;
@@ -254,17 +291,17 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
     if (f >= a.nframes) return;
     const int nc = min(C, N1 - c0);
     float2* b0 = glds;
-    float2* b1 = glds + nc * N2;
     // rows of nc contiguous samples (lanes walk the column)
     for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
-        const int n2 = p / nc, col = p - n2 * nc;
+        const int n2 = small_div(p, nc), col = p - n2 * nc;
         b0[col * N2 + n2] = frame_sample(a.src, a.N, f, (long)(c0 + col) + (long)N1 * n2);
     }
     __syncthreads();
-    const float2* X = gen_engine(b0, b1, N2, nc, a.rlA, a.twA);
+    gen_engine(b0, N2, nc, a.rlA, a.twA);
+    const float2* X = b0;
     float2* S = a.scratch + f * (long)a.N + (long)c0 * N2;
     for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
-        const int col = p / N2, k2 = p - col * N2;
+        const int col = a.rlA.dn.div(p), k2 = p - col * N2;
         S[p] = cmul(X[p], a.twN[(c0 + col) * k2]);   // (n1 k2 < N)
     }
 }
@@ -279,16 +316,16 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_b(Gen4Args a) {
     if (f >= a.nframes) return;
     const int nc = min(C, N2 - c0);
     float2* b0 = glds;
-    float2* b1 = glds + nc * N1;
     const float2* S = a.scratch + f * (long)a.N;
     for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
-        const int n1 = p / nc, col = p - n1 * nc;
+        const int n1 = small_div(p, nc), col = p - n1 * nc;
         b0[col * N1 + n1] = S[(long)n1 * N2 + c0 + col];
     }
     __syncthreads();
-    const float2* X = gen_engine(b0, b1, N1, nc, a.rlB, a.twB);
+    gen_engine(b0, N1, nc, a.rlB, a.twB);
+    const float2* X = b0;
     for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
-        const int k1 = p / nc, col = p - k1 * nc;
+        const int k1 = small_div(p, nc), col = p - k1 * nc;
         const long k = (long)(c0 + col) + (long)N2 * k1;
         store_bin(a.out, f, a.N, k, X[col * N1 + k1], a.store_mode, a.norm);
     }
@@ -360,7 +397,16 @@ bool radices(int n, RadixList& rl) {
             n /= p;
         }
     }
-    return n == 1;
+    if (n != 1) return false;
+    int N = 1, Ns = 1;
+    for (int i = 0; i < rl.n; ++i) N *= rl.R[i];
+    for (int i = 0; i < rl.n; ++i) {
+        rl.dq[i].set(N / rl.R[i]);
+        rl.dns[i].set(Ns);
+        Ns *= rl.R[i];
+    }
+    rl.dn.set(N);
+    return true;
 }
 
 std::vector<float2> twiddles(long n) {
@@ -527,7 +573,7 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         a.out = out;
         const long blocks = (fr.nframes + a.B - 1) / a.B;
         hipLaunchKernelGGL(gen_tile_kernel, dim3((unsigned)blocks), dim3(kGenBlock),
-                           2 * (size_t)a.B * N * sizeof(float2), s, a);
+                           (size_t)a.B * N * sizeof(float2), s, a);
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
     }
@@ -554,10 +600,10 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
             a.nframes = nf;
             a.out = store_advance(out, f0, N, store_mode);
             hipLaunchKernelGGL(gen4_pass_a, dim3((unsigned)(nf * ta)), dim3(kGenBlock),
-                               2 * (size_t)std::min(CA, p->N1) * p->N2 * sizeof(float2), s, a);
+                               (size_t)std::min(CA, p->N1) * p->N2 * sizeof(float2), s, a);
             SDRGPU_LAUNCH_CHECK();
             hipLaunchKernelGGL(gen4_pass_b, dim3((unsigned)(nf * tb)), dim3(kGenBlock),
-                               2 * (size_t)std::min(CB, p->N2) * p->N1 * sizeof(float2), s, a);
+                               (size_t)std::min(CB, p->N2) * p->N1 * sizeof(float2), s, a);
             SDRGPU_LAUNCH_CHECK();
         }
         return SDRGPU_OK;

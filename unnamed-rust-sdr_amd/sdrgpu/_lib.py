@@ -126,6 +126,8 @@ SIGNATURES = [
     ("sdrgpu_fft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_fft_exec_dev", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_rfft_exec", c_int, [_H, c_void_p, c_void_p, c_size_t]),
+
+    ("sdrgpu_rfft_exec_dev", c_int, [_H, c_void_p, c_void_p, c_size_t]),
     ("sdrgpu_fft_set_output", c_int, [_H, c_int]),
     ("sdrgpu_fft_sync", c_int, [_H]),
     ("sdrgpu_fft_destroy", None, [_H]),

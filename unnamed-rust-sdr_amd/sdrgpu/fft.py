@@ -87,6 +87,10 @@ class FftPlan:
     def exec_dev(self, d_in: int, d_out: int, count: int):
         check(lib().sdrgpu_fft_exec_dev(self._h, d_in, d_out, count), "sdrgpu_fft_exec_dev")
 
+    def exec_real_dev(self, d_in: int, d_out: int, count: int):
+        """rfft of `count` device-resident frames (n f32 each) -> n - n/2 outputs per frame."""
+        check(lib().sdrgpu_rfft_exec_dev(self._h, d_in, d_out, count), "sdrgpu_rfft_exec_dev")
+
     def sync(self):
         check(lib().sdrgpu_fft_sync(self._h), "sdrgpu_fft_sync")
 
