@@ -329,8 +329,12 @@ void sdrgpu_biquad_destroy(sdrgpu_biquad* h);
  *
  * Converters: SDRGPU_SRC_ZERO_ORDER_HOLD and SDRGPU_SRC_LINEAR follow libsamplerate's
  * src_zoh.c / src_linear.c exactly (f64 position walk, f32 samples, state carried across
- * calls).  The three sinc converters need libsamplerate's coefficient tables, which are not
- * in this image: sdrgpu_src_new returns SRC_ERR_BAD_CONVERTER for them.
+ * calls).  The three sinc converters follow libsamplerate 0.2's src_sinc.c (buffer
+ * handling, fixed-point filter index, ratio ramp, end-of-input flush, f64 sums) with our own
+ * Kaiser-windowed sinc tables of libsamplerate's increments and lengths -- its coefficient
+ * headers are not in this image, so their outputs are not libsamplerate's.
+ * end_of_input is honoured as there (the Rust wrapper sets it for an empty input slice,
+ * whose pointer is non-NULL: pass a non-NULL data_in to flush).
  *
  * Frames hold `channels` interleaved f32 (f32 = 1, Complex<f32> = 2, (A, B) = sum;
  * src/resample.rs:272-282); a large channel count batches many independent streams that
@@ -354,6 +358,7 @@ enum sdrgpu_src_error {           /* libsamplerate's codes, as src/resample.rs:2
     SDRGPU_SRC_ERR_BAD_CONVERTER = 10,
     SDRGPU_SRC_ERR_BAD_CHANNEL_COUNT = 11,
     SDRGPU_SRC_ERR_DATA_OVERLAP = 16,
+    SDRGPU_SRC_ERR_SINC_PREPARE_DATA_BAD_LEN = 21,
     SDRGPU_SRC_ERR_BAD_INTERNAL_STATE = 22,
 };
 /* layout of libsamplerate's SRC_DATA (the struct SampleRate::process fills, :47-56) */
@@ -382,6 +387,10 @@ const char* sdrgpu_src_strerror(int error);
 const char* sdrgpu_src_get_name(int converter_type);        /* NULL for unknown ids */
 const char* sdrgpu_src_get_description(int converter_type);
 const char* sdrgpu_src_get_version(void);
+/* The coefficient table of sinc converter 0..2 (length returned; coeffs == NULL asks for
+ * the length only; *increment = the table's index increment).  -1 for other ids or a
+ * short buffer.  Not in libsamplerate's API: the tables are this library's own. */
+int sdrgpu_src_sinc_table(int converter_type, float* coeffs, int cap, int* increment);
 
 /* =====================================================================================
  * Multi-GPU channel sharding (configs[4]: channels sharded across the GPUs of one node).

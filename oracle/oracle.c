@@ -547,11 +547,18 @@ void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
  * src/resample.rs:46-67 fills an SRC_DATA and calls src_process; restated here are
  * samplerate.c's src_process checks and src_zoh.c / src_linear.c's process loops, counting
  * in samples (frames x channels) as those files do. */
+typedef struct sinc_filter sinc_filter;
 struct oracle_src {
     int converter, channels, reset;
     double last_ratio, last_position;
     float* last_value;
+    sinc_filter* sinc; /* converters 0..2 */
 };
+static sinc_filter* sinc_new(int converter, int channels);
+static void sinc_free(sinc_filter* f);
+static void sinc_reset(sinc_filter* f);
+static int sinc_process(oracle_src* s, const float* in, long in_frames, float* out,
+                        long out_frames, double ratio, long* in_used_frames, long* out_gen_frames);
 
 static double src_fmod_one(double x) {
     double res = x - lrint(x);
@@ -563,18 +570,20 @@ static int src_bad_ratio(double r) { return r < (1.0 / 256.0) || r > 256.0; }
 
 oracle_src* oracle_src_new(int converter, int channels, int* error) {
     *error = 0;
-    if (converter != 3 && converter != 4) { *error = 10; return NULL; }
+    if (converter < 0 || converter > 4) { *error = 10; return NULL; }
     if (channels < 1) { *error = 11; return NULL; }
     oracle_src* s = (oracle_src*)calloc(1, sizeof(*s));
     s->converter = converter;
     s->channels = channels;
     s->last_value = (float*)calloc((size_t)channels, sizeof(float));
+    if (converter <= 2) s->sinc = sinc_new(converter, channels);
     oracle_src_reset(s);
     return s;
 }
 
 void oracle_src_delete(oracle_src* s) {
     if (!s) return;
+    sinc_free(s->sinc);
     free(s->last_value);
     free(s);
 }
@@ -584,6 +593,7 @@ int oracle_src_reset(oracle_src* s) {
     memset(s->last_value, 0, sizeof(float) * (size_t)s->channels);
     s->last_position = 0.0;
     s->last_ratio = 0.0;
+    if (s->sinc) sinc_reset(s->sinc);
     return 0;
 }
 
@@ -602,6 +612,8 @@ int oracle_src_process(oracle_src* s, const float* in, long in_frames, float* ou
     if (in_frames < 0) in_frames = 0;
     if (out_frames < 0) out_frames = 0;
     if (s->last_ratio < (1.0 / 256.0)) s->last_ratio = ratio;
+    if (s->sinc) return sinc_process(s, in, in_frames, out, out_frames, ratio, in_used_frames,
+                                     out_gen_frames);
     /* converter process loop */
     if (in_frames <= 0) return 0;
     const int ch = s->channels, linear = s->converter == 4;
@@ -665,5 +677,256 @@ int oracle_src_process(oracle_src* s, const float* in, long in_frames, float* ou
     s->last_ratio = src_ratio;
     *in_used_frames = in_used / ch;
     *out_gen_frames = out_gen / ch;
+    return 0;
+}
+
+/* ======================= sinc converters (libsamplerate src_sinc.c) ===================
+ * SincBestQuality / SincMediumQuality / SincFastest (ids 0 / 1 / 2, src/resample.rs:
+ * 112-149; src/main.rs:50 uses SincFastest, Signal::resample SincBestQuality,
+ * src/signal/mod.rs:78-84).  Restated from libsamplerate 0.2's published src_sinc.c:
+ * sinc_set_converter (buffer length), sinc_reset, prepare_data (the input ring with its
+ * zero lead-in, memmove compaction and end-of-input zero tail), the vari process loop
+ * (fixed-point filter index, 12 fraction bits; ratio ramp; termination) and
+ * calc_output_multi (left half walked outward-in, right half inward-out, each tap's
+ * coefficient linearly interpolated between table entries, f64 accumulation).
+ *
+ * The coefficient TABLES of libsamplerate (fastest_coeffs.h, mid_qual_coeffs.h,
+ * high_qual_coeffs.h) are not in this image; the tables here keep their increments and
+ * lengths (128 / 2464, 491 / 22438, 2381 / 340239) and are our own Kaiser-windowed sincs
+ * (oracle_sinc_table).  So outputs follow libsamplerate's algorithm with a different
+ * low-pass: parity is UNPINNED for the sinc converters. */
+
+#define SINC_SHIFT_BITS 12
+#define SINC_FP_ONE ((double)(1 << SINC_SHIFT_BITS))
+#define SINC_INV_FP_ONE (1.0 / SINC_FP_ONE)
+
+static const struct { int inc, len; double atten_db; } k_sinc_spec[3] = {
+    {2381, 340239, 144.0}, /* best    */
+    {491, 22438, 121.0},   /* medium  */
+    {128, 2464, 97.0},     /* fastest */
+};
+
+static double bessel_i0(double x) {
+    double sum = 1.0, term = 1.0, q = 0.25 * x * x;
+    for (int k = 1; k < 500; k++) {
+        term *= q / ((double)k * (double)k);
+        sum += term;
+        if (term < 1e-17 * sum) break;
+    }
+    return sum;
+}
+
+/* Kaiser-windowed sinc sampled at t = i / inc input samples (i < len; zero at and beyond
+ * the half length T = (len - 2) / inc).  Kaiser's formulas for attenuation A over the
+ * window length 2T: transition width dw = (A - 8) / (2.285 * 2T) rad/sample, stopband edge
+ * at Nyquist, cutoff fc = 1 - dw / (2 pi) (Nyquist units), beta = 0.1102 (A - 8.7); the
+ * table is scaled so the integer-spaced taps sum to 1 (unit DC gain at ratio >= 1). */
+int oracle_sinc_table(int converter, float* out, int cap, int* increment) {
+    if (converter < 0 || converter > 2) return -1;
+    const int inc = k_sinc_spec[converter].inc, len = k_sinc_spec[converter].len;
+    if (increment) *increment = inc;
+    if (!out) return len;
+    if (cap < len) return -1;
+    const double A = k_sinc_spec[converter].atten_db;
+    const double T = (double)(len - 2) / (double)inc;
+    const double dw = (A - 8.0) / (2.285 * 2.0 * T);
+    const double fc = 1.0 - dw / (2.0 * M_PI);
+    const double beta = 0.1102 * (A - 8.7), i0b = bessel_i0(beta);
+    double* h = (double*)malloc(sizeof(double) * (size_t)len);
+    if (!h) return -1;
+    for (int i = 0; i < len; i++) {
+        const double t = (double)i / (double)inc;
+        if (t >= T) { h[i] = 0.0; continue; }
+        const double x = t / T;
+        const double w = bessel_i0(beta * sqrt(1.0 - x * x)) / i0b;
+        const double s = i == 0 ? fc : sin(M_PI * fc * t) / (M_PI * t);
+        h[i] = s * w;
+    }
+    double g = len > 0 ? h[0] : 1.0;
+    for (int i = inc; i < len; i += inc) g += 2.0 * h[i];
+    for (int i = 0; i < len; i++) out[i] = (float)(h[i] / g);
+    free(h);
+    return len;
+}
+
+struct sinc_filter {
+    int channels;
+    long in_count, in_used, out_count, out_gen;
+    int coeff_half_len, index_inc;
+    float* coeffs;
+    int b_current, b_end, b_real_end, b_len;
+    float* buffer; /* b_len + channels */
+    double *left, *right;
+};
+
+static sinc_filter* sinc_new(int converter, int channels) {
+    sinc_filter* f = (sinc_filter*)calloc(1, sizeof(*f));
+    int inc = 0;
+    const int len = oracle_sinc_table(converter, NULL, 0, &inc);
+    f->channels = channels;
+    f->coeffs = (float*)malloc(sizeof(float) * (size_t)len);
+    oracle_sinc_table(converter, f->coeffs, len, &inc);
+    f->coeff_half_len = len - 2; /* ARRAY_LEN (coeffs) - 2 */
+    f->index_inc = inc;
+    /* sinc_set_converter */
+    int b_len = 3 * (int)lrint((f->coeff_half_len + 2.0) / f->index_inc * 256.0 + 1);
+    if (b_len < 4096) b_len = 4096;
+    b_len *= channels;
+    b_len += 1;
+    f->b_len = b_len;
+    f->buffer = (float*)calloc((size_t)(b_len + channels), sizeof(float));
+    f->left = (double*)calloc((size_t)channels, sizeof(double));
+    f->right = (double*)calloc((size_t)channels, sizeof(double));
+    sinc_reset(f);
+    return f;
+}
+
+static void sinc_free(sinc_filter* f) {
+    if (!f) return;
+    free(f->coeffs);
+    free(f->buffer);
+    free(f->left);
+    free(f->right);
+    free(f);
+}
+
+static void sinc_reset(sinc_filter* f) {
+    f->b_current = f->b_end = 0;
+    f->b_real_end = -1;
+    memset(f->buffer, 0, sizeof(float) * (size_t)f->b_len);
+}
+
+/* prepare_data: fill the buffer from data_in (never NULL from Rust; end_of_input is
+ * input.len() == 0, src/resample.rs:53). */
+static int sinc_prepare_data(sinc_filter* f, const float* in, int end_of_input, int half) {
+    const int ch = f->channels;
+    int len = 0;
+    if (f->b_real_end >= 0) return 0; /* terminating */
+    if (f->b_current == 0) {
+        len = f->b_len - 2 * half; /* initial: zeros lead in, load after them */
+        f->b_current = f->b_end = half;
+    } else if (f->b_end + half + ch < f->b_len) {
+        len = f->b_len - f->b_current - half;
+        if (len < 0) len = 0;
+    } else {
+        len = f->b_end - f->b_current;
+        if (f->b_current - half < 0) return 21; /* would read before the buffer */
+        memmove(f->buffer, f->buffer + f->b_current - half, sizeof(float) * (size_t)(half + len));
+        f->b_current = half;
+        f->b_end = f->b_current + len;
+        len = f->b_len - f->b_current - half;
+        if (len < 0) len = 0;
+    }
+    if ((long)len > f->in_count - f->in_used) len = (int)(f->in_count - f->in_used);
+    len -= len % ch;
+    if (len < 0 || f->b_end + len > f->b_len) return 21; /* SINC_PREPARE_DATA_BAD_LEN */
+    if (len) memcpy(f->buffer + f->b_end, in + f->in_used, sizeof(float) * (size_t)len);
+    f->b_end += len;
+    f->in_used += len;
+    if (f->in_used == f->in_count && f->b_end - f->b_current < 2 * half && end_of_input) {
+        if (f->b_len - f->b_end < half + 5) {
+            len = f->b_end - f->b_current;
+            if (f->b_current - half < 0) return 21;
+            memmove(f->buffer, f->buffer + f->b_current - half, sizeof(float) * (size_t)(half + len));
+            f->b_current = half;
+            f->b_end = f->b_current + len;
+        }
+        f->b_real_end = f->b_end;
+        len = half + 5;
+        if (len < 0 || f->b_end + len > f->b_len) len = f->b_len - f->b_end;
+        memset(f->buffer + f->b_end, 0, sizeof(float) * (size_t)len);
+        f->b_end += len;
+    }
+    return 0;
+}
+
+/* calc_output_multi: one output frame at b_current + input_index */
+static void sinc_calc_output(sinc_filter* f, int increment, int start_filter_index,
+                             double scale, float* out) {
+    const int ch = f->channels;
+    const int max_filter_index = f->coeff_half_len << SINC_SHIFT_BITS;
+    const float* c = f->coeffs;
+    /* left half */
+    int filter_index = start_filter_index;
+    int coeff_count = (max_filter_index - filter_index) / increment;
+    filter_index = filter_index + coeff_count * increment;
+    int data_index = f->b_current - ch * coeff_count;
+    if (data_index < 0) { /* avoid reading before the buffer */
+        const int steps = (-data_index + ch - 1) / ch;
+        filter_index -= increment * steps;
+        data_index += steps * ch;
+    }
+    for (int k = 0; k < ch; k++) f->left[k] = 0.0;
+    while (filter_index >= 0) {
+        const double fraction = (double)(filter_index & ((1 << SINC_SHIFT_BITS) - 1)) * SINC_INV_FP_ONE;
+        const int indx = filter_index >> SINC_SHIFT_BITS;
+        const double icoeff = c[indx] + fraction * (c[indx + 1] - c[indx]);
+        for (int k = 0; k < ch; k++) f->left[k] += icoeff * f->buffer[data_index + k];
+        filter_index -= increment;
+        data_index = data_index + ch;
+    }
+    /* right half */
+    filter_index = increment - start_filter_index;
+    coeff_count = (max_filter_index - filter_index) / increment;
+    filter_index = filter_index + coeff_count * increment;
+    data_index = f->b_current + ch * (1 + coeff_count);
+    for (int k = 0; k < ch; k++) f->right[k] = 0.0;
+    do {
+        const double fraction = (double)(filter_index & ((1 << SINC_SHIFT_BITS) - 1)) * SINC_INV_FP_ONE;
+        const int indx = filter_index >> SINC_SHIFT_BITS;
+        const double icoeff = c[indx] + fraction * (c[indx + 1] - c[indx]);
+        for (int k = 0; k < ch; k++) f->right[k] += icoeff * f->buffer[data_index + k];
+        filter_index -= increment;
+        data_index = data_index - ch;
+    } while (filter_index > 0);
+    for (int k = 0; k < ch; k++) out[k] = (float)(scale * (f->left[k] + f->right[k]));
+}
+
+/* sinc_multichan_vari_process (const and vari process are the same loop) */
+static int sinc_process(oracle_src* s, const float* in, long in_frames, float* out,
+                        long out_frames, double ratio, long* in_used_frames, long* out_gen_frames) {
+    sinc_filter* f = s->sinc;
+    const int ch = f->channels;
+    f->in_count = in_frames * ch;
+    f->out_count = out_frames * ch;
+    f->in_used = f->out_gen = 0;
+    double src_ratio = s->last_ratio;
+    if (src_bad_ratio(src_ratio)) return 22;
+    double count = (f->coeff_half_len + 2.0) / f->index_inc;
+    const double rmin = s->last_ratio < ratio ? s->last_ratio : ratio;
+    if (rmin < 1.0) count /= rmin;
+    const int half = ch * ((int)lrint(count) + 1);
+    double input_index = s->last_position;
+    double rem = src_fmod_one(input_index);
+    f->b_current = (f->b_current + ch * (int)lrint(input_index - rem)) % f->b_len;
+    input_index = rem;
+    const double terminate = 1.0 / src_ratio + 1e-20;
+    const int end_of_input = in_frames == 0;
+    while (f->out_gen < f->out_count) {
+        int in_hand = (f->b_end - f->b_current + f->b_len) % f->b_len;
+        if (in_hand <= half) {
+            const int err = sinc_prepare_data(f, in, end_of_input, half);
+            if (err) return err;
+            in_hand = (f->b_end - f->b_current + f->b_len) % f->b_len;
+            if (in_hand <= half) break;
+        }
+        if (f->b_real_end >= 0 && f->b_current + input_index + terminate > f->b_real_end) break;
+        if (f->out_count > 0 && fabs(s->last_ratio - ratio) > 1e-10)
+            src_ratio = s->last_ratio + f->out_gen * (ratio - s->last_ratio) / f->out_count;
+        const double float_increment = f->index_inc * (src_ratio < 1.0 ? src_ratio : 1.0);
+        const int increment = (int)lrint(float_increment * SINC_FP_ONE);
+        const int start_filter_index = (int)lrint(input_index * float_increment * SINC_FP_ONE);
+        sinc_calc_output(f, increment, start_filter_index, float_increment / f->index_inc,
+                         out + f->out_gen);
+        f->out_gen += ch;
+        input_index += 1.0 / src_ratio;
+        rem = src_fmod_one(input_index);
+        f->b_current = (f->b_current + ch * (int)lrint(input_index - rem)) % f->b_len;
+        input_index = rem;
+    }
+    s->last_position = input_index;
+    s->last_ratio = src_ratio;
+    *in_used_frames = f->in_used / ch;
+    *out_gen_frames = f->out_gen / ch;
     return 0;
 }

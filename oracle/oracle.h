@@ -98,7 +98,7 @@ size_t oracle_stft(const float* in, size_t n_in, size_t n, size_t hop, float* ou
  * version unpinned) restated from its published src_zoh.c / src_linear.c / samplerate.c:
  * src_new + src_process (argument checks, last_ratio priming) + the converter's process
  * loop (f64 position walk, f32 samples, last_value carried across calls), src_reset,
- * src_set_ratio.  Converter ids: 3 = ZERO_ORDER_HOLD, 4 = LINEAR (others -> error 10).
+ * src_set_ratio.  Converter ids: 0..2 = sinc (below), 3 = ZERO_ORDER_HOLD, 4 = LINEAR.
  * Parity unpinned: no libsamplerate outputs are available here. */
 typedef struct oracle_src oracle_src;
 oracle_src* oracle_src_new(int converter, int channels, int* error);
@@ -108,6 +108,12 @@ int  oracle_src_set_ratio(oracle_src* s, double ratio);
 /* SRC_DATA's fields as arguments; returns the libsamplerate error code */
 int  oracle_src_process(oracle_src* s, const float* in, long in_frames, float* out,
                         long out_frames, double ratio, long* in_used, long* out_gen);
+
+/* Sinc converters 0 / 1 / 2 (Best / Medium / Fastest) follow libsamplerate 0.2's src_sinc.c
+ * with our own Kaiser-windowed sinc tables of libsamplerate's increments and lengths (its
+ * coefficient headers are absent): parity unpinned.  oracle_sinc_table writes the table
+ * (returns its length; out == NULL asks for the length only) and its increment. */
+int  oracle_sinc_table(int converter, float* out, int cap, int* increment);
 
 /* ---------------- Sources (src/signal/sources.rs) ------------------------------- */
 /* freq(rate, f, phase) (sources.rs:196-221 via FreqSweep::next :150-175), n samples */

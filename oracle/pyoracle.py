@@ -69,6 +69,7 @@ def lib():
         L.oracle_src_new.restype = c_void_p
         L.oracle_src_new.argtypes = [c_int, c_int, POINTER(c_int)]
         L.oracle_src_delete.argtypes = [c_void_p]
+        L.oracle_sinc_table.argtypes = [c_int, c_void_p, c_int, POINTER(c_int)]
         L.oracle_src_reset.argtypes = [c_void_p]
         L.oracle_src_set_ratio.argtypes = [c_void_p, ctypes.c_double]
         L.oracle_src_process.argtypes = [c_void_p, c_void_p, ctypes.c_long, c_void_p,
@@ -208,8 +209,17 @@ def u8_to_c64(iq_u8):
     return out
 
 
+def sinc_table(converter):
+    """(coefficients f32, increment) of sinc converter 0/1/2 (oracle_sinc_table)."""
+    inc = c_int(0)
+    n = lib().oracle_sinc_table(converter, None, 0, ctypes.byref(inc))
+    out = np.empty(n, np.float32)
+    lib().oracle_sinc_table(converter, out.ctypes.data, n, ctypes.byref(inc))
+    return out, inc.value
+
+
 class SampleRate:
-    """libsamplerate ZOH / linear restatement behind SampleRate (src/resample.rs:32-110).
+    """libsamplerate sinc / ZOH / linear restatement behind SampleRate (src/resample.rs:32-110).
 
     `process(ratio, frames)` takes a (n, channels) float32 array and returns
     (input_frames_used, output (m, channels)), like SampleRate::process with an output

@@ -12,6 +12,7 @@
 // the L / f table is a per-frame broadcast.  HBM bound: 4 B in (+ neighbour reuse from L2)
 // + 4 B out per sample.
 #include "common.hpp"
+#include "resample_kernels.hpp"
 
 namespace sdrgpu {
 
@@ -105,6 +106,80 @@ int src_interp_launch(bool linear, const float* in, long channels, const int* le
         src_launch_t<true>(in, channels, left, frac, nframes, last_value, out, s);
     else
         src_launch_t<false>(in, channels, left, frac, nframes, last_value, out, s);
+    return hipGetLastError() == hipSuccess ? SDRGPU_OK : SDRGPU_ERR_LAUNCH;
+}
+
+
+// ---- sinc converters (libsamplerate src_sinc.c calc_output_multi) ----------------------
+// The host (abi_resample.cpp) restates src_sinc.c's buffer bookkeeping (prepare_data, the
+// fixed-point filter index, the ratio ramp, termination) over integers only and hands each
+// output frame a descriptor: where its left half starts (window sample index + filter
+// index, after libsamplerate's underflow skip), where its right half starts, the tap
+// counts, the fixed-point increment and the output scale.  This kernel evaluates
+//     left  = sum over the left taps  (data index ascending)  of icoeff * x
+//     right = sum over the right taps (data index descending) of icoeff * x
+//     icoeff = c[i] + frac * (c[i+1] - c[i])   (f32 difference, f64 product and sum)
+//     out   = (float)(scale * (left + right))
+// in that f64 order with explicit round-to-nearest ops, one (frame, channel) per lane, so
+// outputs are bit-identical to the restatement.  The window holds the stream samples the
+// libsamplerate buffer would hold (channel-interleaved), so lanes of one frame read
+// consecutive channels.  Per output ~2 * half_len / increment taps (SincFastest at ratio
+// 0.08: ~480): FP64-issue bound, not HBM bound.
+
+
+namespace {
+
+__device__ __forceinline__ double sinc_icoeff(const float* __restrict__ c, int fi) {
+    const double frac = (double)(fi & 4095) * (1.0 / 4096.0);
+    const int i = fi >> 12;
+    const float c0 = c[i], c1 = c[i + 1];
+    return __dadd_rn((double)c0, __dmul_rn(frac, (double)__fsub_rn(c1, c0)));
+}
+
+template <int CH>
+__global__ __launch_bounds__(kSrcBlock) void src_sinc_kernel(
+    const float* __restrict__ win, long channels, const SincDesc* __restrict__ desc,
+    long nframes, const float* __restrict__ coeffs, float* __restrict__ out) {
+    const long C = CH > 0 ? CH : channels;
+    const long total = nframes * C;
+    const long stride = (long)gridDim.x * kSrcBlock;
+    for (long t = (long)blockIdx.x * kSrcBlock + threadIdx.x; t < total; t += stride) {
+        const long k = CH > 0 ? t / CH : (long)((unsigned long)t / (unsigned long)C);
+        const long ch = t - k * C;
+        const SincDesc d = desc[k];
+        double left = 0.0, right = 0.0;
+        int fi = d.fil;
+        long x = (long)d.dl + ch;
+        for (int n = 0; n < d.nl; ++n) {
+            left = __dadd_rn(left, __dmul_rn(sinc_icoeff(coeffs, fi), (double)win[x]));
+            fi -= d.inc;
+            x += C;
+        }
+        fi = d.fir;
+        x = (long)d.dr + ch;
+        for (int n = 0; n < d.nr; ++n) {
+            right = __dadd_rn(right, __dmul_rn(sinc_icoeff(coeffs, fi), (double)win[x]));
+            fi -= d.inc;
+            x -= C;
+        }
+        out[t] = (float)__dmul_rn(d.scale, __dadd_rn(left, right));
+    }
+}
+
+}  // namespace
+
+int src_sinc_launch(const float* win, long channels, const SincDesc* desc, long nframes,
+                    const float* coeffs, float* out, hipStream_t s) {
+    if (nframes <= 0 || channels <= 0) return SDRGPU_OK;
+    long blocks = (nframes * channels + kSrcBlock - 1) / kSrcBlock;
+    if (blocks > 65536) blocks = 65536;
+    const unsigned g = (unsigned)blocks;
+    if (channels == 1)
+        src_sinc_kernel<1><<<g, kSrcBlock, 0, s>>>(win, 1, desc, nframes, coeffs, out);
+    else if (channels == 2)
+        src_sinc_kernel<2><<<g, kSrcBlock, 0, s>>>(win, 2, desc, nframes, coeffs, out);
+    else
+        src_sinc_kernel<0><<<g, kSrcBlock, 0, s>>>(win, channels, desc, nframes, coeffs, out);
     return hipGetLastError() == hipSuccess ? SDRGPU_OK : SDRGPU_ERR_LAUNCH;
 }
 

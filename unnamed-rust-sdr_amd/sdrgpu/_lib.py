@@ -188,6 +188,7 @@ SIGNATURES = [
     ("sdrgpu_src_get_name", c_char_p, [c_int]),
     ("sdrgpu_src_get_description", c_char_p, [c_int]),
     ("sdrgpu_src_get_version", c_char_p, []),
+    ("sdrgpu_src_sinc_table", c_int, [c_int, c_void_p, c_int, POINTER(c_int)]),
     # multi-GPU fan-out / gather (RCCL)
     ("sdrgpu_comm_unique_id", c_int, [c_void_p]),
     ("sdrgpu_comm_init", c_int, [c_int, c_int, c_int, c_void_p, _PH]),

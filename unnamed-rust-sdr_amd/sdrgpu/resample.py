@@ -3,9 +3,11 @@
 `SampleRate` keeps the reference's surface -- new(ConverterType), process(ratio, input,
 out_cap) -> (input_used, output), reset(), try_clone(), channels(), set_ratio(), and the
 Error enum with libsamplerate's codes (src/resample.rs:151-270) -- on top of the
-`sdrgpu_src_*` C ABI (include/sdrgpu.h), which restates libsamplerate's zero-order-hold and
-linear converters bit-exactly on the GPU.  The sinc converters are rejected with
-Error.BadConverter (their coefficient tables are not available).
+`sdrgpu_src_*` C ABI (include/sdrgpu.h), which restates libsamplerate's converters on the
+GPU: zero-order hold and linear bit-exactly; the sinc converters with libsamplerate 0.2's
+src_sinc.c algorithm over this library's own Kaiser-windowed sinc tables (libsamplerate's
+coefficient headers are not available, so sinc outputs are not libsamplerate's; DESIGN.md
+3.7).
 
 Frames: an input array of shape (n, channels) float32, or 1-D float32 (channels = 1) /
 complex64 (channels = 2, num::Complex<f32> as [f32; 2], src/resample.rs:272-278).
@@ -65,6 +67,20 @@ class SrcData(ctypes.Structure):
                 ("src_ratio", c_double)]
 
 
+_EMPTY = np.zeros(1, np.float32)
+
+
+def sinc_table(typ: ConverterType):
+    """(coefficients f32, increment) of a sinc converter's table (sdrgpu_src_sinc_table)."""
+    inc = c_int(0)
+    n = lib().sdrgpu_src_sinc_table(int(typ), None, 0, ctypes.byref(inc))
+    if n < 0:
+        raise Error(10)
+    out = np.empty(n, np.float32)
+    lib().sdrgpu_src_sinc_table(int(typ), out.ctypes.data, n, ctypes.byref(inc))
+    return out, inc.value
+
+
 def version() -> str:
     """resample::version (src/resample.rs:3-8)."""
     return lib().sdrgpu_src_get_version().decode()
@@ -103,7 +119,11 @@ class SampleRate:
         """SampleRate::process (:46-67): returns (input_frames_used, output frames)."""
         x = _frames(input, self._ch)
         out = np.empty((max(int(out_cap), 1), self._ch), np.float32)
-        d = SrcData(x.ctypes.data if x.shape[0] else None, out.ctypes.data, x.shape[0],
+        # an empty Rust slice has a non-NULL pointer, so src_process sees end_of_input
+        # with data_in set and the sinc converters flush (src/resample.rs:47-56)
+        if not x.shape[0]:
+            x = np.zeros((1, self._ch), np.float32)[:0]
+        d = SrcData(x.ctypes.data or _EMPTY.ctypes.data, out.ctypes.data, x.shape[0],
                     int(out_cap), 0, 0, 1 if x.shape[0] == 0 else 0, float(ratio))
         Error.result(lib().sdrgpu_src_process(self.h, ctypes.byref(d)))
         return d.input_frames_used, out[:d.output_frames_gen].copy()
@@ -111,7 +131,7 @@ class SampleRate:
     def process_dev(self, ratio: float, d_in: int, in_frames: int, d_out: int,
                     out_frames: int):
         """Device-pointer variant: counts return at once, the conversion is enqueued."""
-        d = SrcData(d_in or None, d_out or None, in_frames, out_frames, 0, 0,
+        d = SrcData(d_in or _EMPTY.ctypes.data, d_out or None, in_frames, out_frames, 0, 0,
                     1 if in_frames == 0 else 0, float(ratio))
         Error.result(lib().sdrgpu_src_process_dev(self.h, ctypes.byref(d)))
         return d.input_frames_used, d.output_frames_gen

@@ -16,7 +16,7 @@ reference names and argument meaning:
   .decimate(..).map(fft)  the live.rs STFT pattern -> one GPU Stft stage
   resample(rate), resample_with(typ, rate)
                      adapters::Resample (adapters/resample.rs:17-82): 4096-frame buffers
-                     through resample.SampleRate (GPU ZOH / linear); rate() = the new rate
+                     through resample.SampleRate (GPU sinc / ZOH / linear); rate() = the new rate
   map(f), take(duration), skip(duration), iter(), collect()
 
 Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), freq_sweep
@@ -140,8 +140,8 @@ class Signal:
         return Signal(self._rate, gen, sk)  # Decimate::rate quirk (:38-40)
 
     def resample(self, rate: float) -> "Signal":
-        """Signal::resample (src/signal/mod.rs:78-84): SincBestQuality, which this build
-        rejects with resample.Error(BadConverter) when the stream starts."""
+        """Signal::resample (src/signal/mod.rs:78-84): SincBestQuality (this library's own
+        sinc table)."""
         return self.resample_with(_resample.ConverterType.SincBestQuality, rate)
 
     def resample_with(self, typ, rate: float) -> "Signal":
