@@ -458,30 +458,69 @@ def bench_c5(args):
 
 # ------------------------------------------------------------------------------ src
 def bench_src(args):
-    import sdrgpu
+    """src/main.rs:50's resample_with(SincFastest, 144 kHz) from 1.8 Msps (ratio 0.08) over a
+    batch of 1024 complex streams (2048 interleaved channels), state carried call to call;
+    the linear converter on the same shape; and one mono SincFastest stream (main.rs as
+    written: a single FM audio channel), 4096-frame calls as adapters::Resample makes them."""
+    import time as _t
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
     from sdrgpu import resample
     from sdrgpu.device import DeviceBuffer, synchronize
-    ch, nf = 2048, 1 << 16
     ratio = float(np.float32(144000.0)) / float(np.float32(1.8e6))
-    g = resample.SampleRate(resample.ConverterType.Linear, ch)
-    x = DeviceBuffer.empty(nf * ch // 2)
-    fill(x, nf * ch // 2, 13)
-    out_cap = int(nf * ratio) + 16
-    y = DeviceBuffer.empty(out_cap * ch // 2)
-    gen = [0]
+    lines = []
+    for conv, ch, nf in ((resample.ConverterType.Linear, 2048, 1 << 16),
+                         (resample.ConverterType.SincFastest, 2048, 1 << 16),
+                         (resample.ConverterType.SincFastest, 1, 4096)):
+        g = resample.SampleRate(conv, ch)
+        nfl = nf * ch
+        x = DeviceBuffer.empty((nfl + 1) // 2)
+        fill(x, (nfl + 1) // 2, 13)
+        out_cap = int(nf * ratio) + 16
+        y = DeviceBuffer.empty((out_cap * ch + 1) // 2)
+        gen = [0]
 
-    def step():  # state carries from call to call, as in a stream
-        gen[0] = g.process_dev(ratio, x.ptr, nf, y.ptr, out_cap)[1]
+        def step():  # state carries from call to call, as in a stream
+            gen[0] = g.process_dev(ratio, x.ptr, nf, y.ptr, out_cap)[1]
 
-    wall, ms = time_events(step, g.stream(), args.steps, args.warmup,
-                           lambda: (g.sync(), synchronize()))
-    nout = gen[0]
-    return {"config": "src: linear resampler 1.8 Msps -> 144 kHz (ratio 0.08), 1024 complex "
-                      "streams = 2048 interleaved channels x 2^16 frames",
-            "metric": "input Msamples/s (all channels)", "value": round(nf * ch / (ms * 1e-3) / 1e6, 1),
-            "wall_value": round(nf * ch / wall / 1e6, 1),
-            "output_frames": nout, "wall_ms_per_step": round(wall * 1e3, 3),
-            "roofline_kernel_estimate": roof(12, nout * ch, ms)}
+        wall, ms = time_events(step, g.stream(), args.steps, args.warmup,
+                               lambda: (g.sync(), synchronize()))
+        nout = gen[0]
+        name = "linear" if conv == resample.ConverterType.Linear else "SincFastest"
+        line = {"config": f"src: {name} resampler 1.8 Msps -> 144 kHz (ratio 0.08), "
+                          + (f"{ch // 2} complex streams = {ch} interleaved channels" if ch > 1
+                             else "one mono stream (src/main.rs:50)") + f" x {nf} frames per call",
+                "metric": "input Msamples/s (all channels)",
+                "value": round(nfl / (ms * 1e-3) / 1e6, 1),
+                "wall_value": round(nfl / wall / 1e6, 1),
+                "output_frames": nout, "gpu_ms_per_call": round(ms, 4),
+                "wall_ms_per_step": round(wall * 1e3, 3)}
+        if conv == resample.ConverterType.Linear:
+            line["roofline_kernel_estimate"] = roof(12, nout * ch, ms)
+        else:
+            c, inc = resample.sinc_table(conv)
+            taps = 2 * (c.size - 2) / (inc * ratio)  # per output sample, both halves
+            # per tap per output sample: one f64 multiply + one f64 add (the coefficient
+            # interpolation is per frame, shared by the channels in the wide kernel)
+            fl = 2 * taps * nout * ch / (ms * 1e-3) / 1e12
+            line["taps_per_output"] = round(taps, 1)
+            line["roofline"] = {"bound": "fp64 issue", "achieved": round(fl, 3),
+                                "peak": 78.6, "unit": "TFLOP/s (f64 vector, AMD spec)",
+                                "frac": round(fl / 78.6, 4)}
+            if not args.no_cpu_baseline and ch == 1:
+                xs = np.random.default_rng(1).standard_normal((nf, 1)).astype(np.float32)
+                o = pyoracle.SampleRate(int(conv), 1)
+                t0, done = _t.perf_counter(), 0
+                while _t.perf_counter() - t0 < 3.0:
+                    used, _ = o.process(ratio, xs, out_cap)
+                    done += used
+                dt = _t.perf_counter() - t0
+                line["cpu_baseline"] = {"value": round(done / dt / 1e6, 3),
+                                        "unit": "input Msamples/s", "cores": 1, "kind": "port",
+                                        "sample": f"{done} mono samples through the oracle sinc, {dt:.1f} s"}
+        lines.append(line)
+    return lines
 
 
 def main():

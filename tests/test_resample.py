@@ -255,6 +255,16 @@ def test_src_sinc_bit_exact(sdr, oracle, conv, ratio, ch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ch,ratio", [(100, 48000 * 3.0 / 1.8e6), (64, 2.5), (300, 1 / 200.0)])
+def test_src_sinc_wide_frames(sdr, oracle, ch, ratio):
+    """Wide-frame sinc kernel (>= 64 channels: LDS-staged coefficients, partial channel
+    tiles, tap chunks beyond 1024 at ratio 1/200) against the oracle, ragged blocks."""
+    rng = np.random.default_rng(ch)
+    x = rng.standard_normal((2000 if ratio > 0.01 else 6000, ch)).astype(np.float32)
+    _run_both(sdr, oracle, FASTEST, ch, ratio, x, rng)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("conv", [ZOH, LINEAR, FASTEST], ids=["zoh", "linear", "sinc"])
 def test_src_many_channels_one_shot(sdr, oracle, conv):
     """A batch of 1024 complex streams sharing one ratio = 2048 interleaved channels."""

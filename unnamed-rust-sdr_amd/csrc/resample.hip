@@ -166,11 +166,66 @@ __global__ __launch_bounds__(kSrcBlock) void src_sinc_kernel(
     }
 }
 
+// Wide frames (channels >= 64, a batch of streams sharing one ratio): a workgroup takes one
+// output frame x 256 channels.  The frame's descriptor is uniform, so its interpolated
+// coefficients are computed once per workgroup into LDS (in chunks of kTapChunk taps) and
+// every lane reads them as broadcasts; the tap sums stay sequential per lane (same order,
+// same roundings as the narrow kernel).  Workgroups b, b+8, b+16, ... share an XCD (round-
+// robin placement, speed only): each XCD gets a contiguous range of frames, so the window
+// samples that neighbouring frames share are read from HBM once into that XCD's L2.
+constexpr int kTapChunk = 1024;
+
+__global__ __launch_bounds__(kSrcBlock) void src_sinc_wide_kernel(
+    const float* __restrict__ win, long channels, const SincDesc* __restrict__ desc,
+    long nframes, const float* __restrict__ coeffs, float* __restrict__ out, int ntiles,
+    long per_xcd) {
+    __shared__ double ic[kTapChunk];
+    const long b = blockIdx.x;
+    const long logical = (b & 7) * per_xcd + (b >> 3);
+    if (logical >= nframes * ntiles) return;  // whole workgroup: no barrier is skipped
+    const long k = logical / ntiles;
+    const long ch = (logical - k * ntiles) * kSrcBlock + threadIdx.x;
+    const bool on = ch < channels;
+    const SincDesc d = desc[k];
+    double acc[2] = {0.0, 0.0};
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const int n = side ? d.nr : d.nl, fi0 = side ? d.fir : d.fil;
+        const long step = side ? -channels : channels;
+        long x = (long)(side ? d.dr : d.dl) + ch;
+        double a = 0.0;
+        for (int base = 0; base < n; base += kTapChunk) {
+            const int m = n - base < kTapChunk ? n - base : kTapChunk;
+            for (int j = threadIdx.x; j < m; j += kSrcBlock)
+                ic[j] = sinc_icoeff(coeffs, fi0 - (base + j) * d.inc);
+            __syncthreads();
+            if (on) {
+#pragma unroll 4
+                for (int j = 0; j < m; ++j) {
+                    a = __dadd_rn(a, __dmul_rn(ic[j], (double)win[x]));
+                    x += step;
+                }
+            }
+            __syncthreads();
+        }
+        acc[side] = a;
+    }
+    if (on) out[k * channels + ch] = (float)__dmul_rn(d.scale, __dadd_rn(acc[0], acc[1]));
+}
+
 }  // namespace
 
 int src_sinc_launch(const float* win, long channels, const SincDesc* desc, long nframes,
                     const float* coeffs, float* out, hipStream_t s) {
     if (nframes <= 0 || channels <= 0) return SDRGPU_OK;
+    if (channels >= 64) {
+        const int ntiles = (int)((channels + kSrcBlock - 1) / kSrcBlock);
+        const long per_xcd = (nframes * ntiles + 7) / 8;
+        if (8 * per_xcd > 0x7fffffffL) return SDRGPU_ERR_UNSUPPORTED;
+        src_sinc_wide_kernel<<<(unsigned)(8 * per_xcd), kSrcBlock, 0, s>>>(
+            win, channels, desc, nframes, coeffs, out, ntiles, per_xcd);
+        return hipGetLastError() == hipSuccess ? SDRGPU_OK : SDRGPU_ERR_LAUNCH;
+    }
     long blocks = (nframes * channels + kSrcBlock - 1) / kSrcBlock;
     if (blocks > 65536) blocks = 65536;
     const unsigned g = (unsigned)blocks;
