@@ -107,14 +107,12 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
     const int fpt = kTile / M;  // frames per tile
     const long f0 = (long)blockIdx.x * fpt;
     const int nf = (int)min((long)fpt, a.nframes - f0);
-    // coalesced load: point p -> (frame p / M, sample p % M)
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int p = t + kFftBlock * i;
-        const int f = p / M, n = p % M;
-        float2 x = make_float2(0.f, 0.f);
-        if (f < nf) x = frame_sample(a.src, M, f0 + f, n);
-        lds[fpad(p)] = x;
+    // coalesced load: point p -> (frame p / M, sample p % M), all 16 loads in flight
+    {
+        float2 v[16];
+        gather_tile<16, kFftBlock>(a.src, M, f0, nf, kTile, [](int p) { return p / M; }, v);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lds[fpad(t + kFftBlock * i)] = v[i];
     }
     __syncthreads();
     tile_fft<M, false>(lds, a.tw);

@@ -43,6 +43,84 @@ __device__ __forceinline__ float2 frame_sample(const FrameSrc& s, long M, long f
     return make_float2(0.f, 0.f);
 }
 
+// Workgroup-uniform fast gather: when frames [f0, f0 + nf) of a workgroup lie wholly inside
+// the input (no history, no zero fill), sample (f, n) of them is base[f * stride + n] with
+// one load type, so a tile's loads can all be in flight at once (frame_sample's per-mode,
+// per-range branches put a vmcnt wait between consecutive loads).
+struct FrameFast {
+    int kind;  // 0: use frame_sample; 1: c64, 2: real f32, 3: rtl_tcp u8 pairs
+    const float2* c;
+    const float* r;
+    const unsigned short* u;
+    long stride;  // samples between consecutive frames
+};
+
+__device__ __forceinline__ FrameFast frame_fast(const FrameSrc& s, long M, long f0, long nf) {
+    FrameFast q{0, nullptr, nullptr, nullptr, M};
+    if (nf <= 0) return q;
+    if (s.mode == 0) {
+        q.kind = 1;
+        q.c = s.in + f0 * M;
+    } else if (s.mode == 2) {
+        q.kind = 2;
+        q.r = s.in_real + f0 * M;
+    } else {
+        const long g0 = s.first_end + f0 * s.hop - M, g1 = s.first_end + (f0 + nf - 1) * s.hop;
+        if (g0 >= 0 && g1 <= s.n_in) {
+            q.kind = s.mode == 3 ? 3 : 1;
+            q.stride = s.hop;
+            if (s.mode == 3) q.u = s.in_u8 + g0;
+            else q.c = s.in + g0;
+        }
+    }
+    return q;
+}
+
+// PER samples per lane, lane-strided over the tile (p = t + BLK u, frame p / M via div):
+// v[u] = sample of point p, or 0 past the tile / the last frame
+template <int PER, int BLK, typename Div>
+__device__ __forceinline__ void gather_tile(const FrameSrc& s, long M, long f0, int nf, int L,
+                                            const Div& div, float2 (&v)[PER]) {
+    const FrameFast q = frame_fast(s, M, f0, nf);
+    const int t = threadIdx.x;
+    if (q.kind == 1) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = t + u * BLK, f = div(p), n = p - f * (int)M;
+            const bool ok = p < L && f < nf;
+            const float2 x = q.c[ok ? f * q.stride + n : 0];
+            v[u] = ok ? x : make_float2(0.f, 0.f);
+        }
+    } else if (q.kind == 2) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = t + u * BLK, f = div(p), n = p - f * (int)M;
+            const bool ok = p < L && f < nf;
+            const float x = q.r[ok ? f * q.stride + n : 0];
+            v[u] = make_float2(ok ? x : 0.f, 0.f);
+        }
+    } else if (q.kind == 3) {
+        unsigned short w[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = t + u * BLK, f = div(p), n = p - f * (int)M;
+            const bool ok = p < L && f < nf;
+            w[u] = q.u[ok ? f * q.stride + n : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = t + u * BLK, f = div(p);
+            v[u] = (p < L && f < nf) ? u8_sample(w[u]) : make_float2(0.f, 0.f);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = t + u * BLK, f = div(p), n = p - f * (int)M;
+            v[u] = (p < L && f < nf) ? frame_sample(s, M, f0 + f, n) : make_float2(0.f, 0.f);
+        }
+    }
+}
+
 // Store modes (bin k of frame f):
 //   0 collated fft: out[(k + M/2) mod M] = X[k] * norm (fft.rs:14-26)
 //   1 rfft: collated [M/2, M) = X[0, M - M/2) * norm (fft.rs:35)

@@ -42,6 +42,9 @@ namespace {
 
 constexpr int kGenBlock = 256;
 constexpr int kGenTile = 4096;   // complex points per LDS buffer
+constexpr int kGenTileW = 1024;  // one-wave tiles (N <= 1024)
+constexpr int kGenTileL = 16384; // one frame per 1024-lane workgroup, <= 128 KiB of LDS
+constexpr int kGenBlockL = 1024;
 constexpr int kMaxPass = 16;
 
 // division by a plan-time constant d < 2^16 for dividends < 2^16: q = umulhi(n, ceil(2^32/d))
@@ -154,11 +157,11 @@ __device__ __forceinline__ void dft_any(float2* v, const float2* __restrict__ tw
 // after a barrier, writes them to buf[f N + (j - k) R + k + r Ns].  One LDS buffer instead of
 // a ping-pong pair doubles the workgroups per CU.  B N <= 4096, so a lane owns at most
 // ceil(4096 / (R 256)) butterflies.
-template <int R>
+template <int R, int BLK, int TILE>
 __device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
                                          const float2* __restrict__ tw, const FastDiv& dq,
                                          const FastDiv& dns) {
-    constexpr int NB = (kGenTile / R + kGenBlock - 1) / kGenBlock;
+    constexpr int NB = (TILE / R + BLK - 1) / BLK;
     const int Q = N / R;
     const int total = B * Q;
     const int step = N / (Ns * R);
@@ -166,7 +169,7 @@ __device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
     int dsto[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-        const int g = threadIdx.x + u * kGenBlock;
+        const int g = threadIdx.x + u * BLK;
         dsto[u] = -1;
         if (g < total) {
             const int f = dq.div(g), j = g - f * Q;
@@ -190,7 +193,9 @@ __device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
     }
 }
 
-// Runs the plan's passes in place over B transforms of size N held in buf.
+// Runs the plan's passes in place over B transforms of size N held in buf (BLK lanes, at
+// most TILE points).
+template <int BLK, int TILE>
 __device__ void gen_engine(float2* buf, int N, int B, const RadixList& rl,
                            const float2* __restrict__ tw) {
     int Ns = 1;
@@ -199,15 +204,15 @@ __device__ void gen_engine(float2* buf, int N, int B, const RadixList& rl,
         const FastDiv& dq = rl.dq[ps];
         const FastDiv& dns = rl.dns[ps];
         switch (R) {
-        case 2: gen_pass<2>(buf, N, B, Ns, tw, dq, dns); break;
-        case 3: gen_pass<3>(buf, N, B, Ns, tw, dq, dns); break;
-        case 4: gen_pass<4>(buf, N, B, Ns, tw, dq, dns); break;
-        case 5: gen_pass<5>(buf, N, B, Ns, tw, dq, dns); break;
-        case 7: gen_pass<7>(buf, N, B, Ns, tw, dq, dns); break;
-        case 8: gen_pass<8>(buf, N, B, Ns, tw, dq, dns); break;
-        case 11: gen_pass<11>(buf, N, B, Ns, tw, dq, dns); break;
-        case 13: gen_pass<13>(buf, N, B, Ns, tw, dq, dns); break;
-        default: gen_pass<16>(buf, N, B, Ns, tw, dq, dns); break;
+        case 2: gen_pass<2, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 3: gen_pass<3, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 4: gen_pass<4, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 5: gen_pass<5, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 7: gen_pass<7, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 8: gen_pass<8, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 11: gen_pass<11, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        case 13: gen_pass<13, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
+        default: gen_pass<16, BLK, TILE>(buf, N, B, Ns, tw, dq, dns); break;
         }
         __syncthreads();
         Ns *= R;
@@ -225,23 +230,33 @@ struct GenTileArgs {
     float2* out;
 };
 
-__global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
+// BLK lanes over B = TILE / N frames: 256 lanes / 4096 points, or for N <= 1024 one wave
+// over 1024 points (the passes' barriers are then single-wave; 8 KiB of LDS per wave)
+template <int BLK, int TILE>
+__global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
     extern __shared__ float2 glds[];
     const int N = a.N, B = a.B, L = B * N;
     float2* b0 = glds;
     const long f0 = (long)blockIdx.x * B;
     const int nf = (int)min((long)B, a.nframes - f0);
-    for (int p = threadIdx.x; p < L; p += kGenBlock) {
-        const int f = a.rl.dn.div(p), n = p - f * N;
-        b0[p] = f < nf ? frame_sample(a.src, N, f0 + f, n) : make_float2(0.f, 0.f);
+    {  // every lane's loads in flight before the first LDS write (unrolled, predicated)
+        constexpr int PER = TILE / BLK;
+        float2 v[PER];
+        gather_tile<PER, BLK>(a.src, N, f0, nf, L, [&](int p) { return a.rl.dn.div(p); }, v);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * BLK;
+            if (p < L) b0[p] = v[u];
+        }
     }
     __syncthreads();
-    gen_engine(b0, N, B, a.rl, a.tw);
+    gen_engine<BLK, TILE>(b0, N, B, a.rl, a.tw);
     const float2* X = b0;
     if (a.store_mode == 0 || a.store_mode == 3) {
         // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o
         const int sh = N - N / 2;
-        for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
+#pragma unroll 4
+        for (int p = threadIdx.x; p < nf * N; p += BLK) {
             const int f = a.rl.dn.div(p), o = p - f * N;
             int k = o + sh;
             if (k >= N) k -= N;
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(kGenBlock) void gen_tile_kernel(GenTileArgs a) {
             else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);
         }
     } else {
-        for (int p = threadIdx.x; p < nf * N; p += kGenBlock) {
+        for (int p = threadIdx.x; p < nf * N; p += BLK) {
             const int f = a.rl.dn.div(p), k = p - f * N;
             store_bin(a.out, f0 + f, N, k, X[p], a.store_mode, a.norm);
         }
@@ -291,13 +306,25 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
     if (f >= a.nframes) return;
     const int nc = min(C, N1 - c0);
     float2* b0 = glds;
-    // rows of nc contiguous samples (lanes walk the column)
-    for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
-        const int n2 = small_div(p, nc), col = p - n2 * nc;
-        b0[col * N2 + n2] = frame_sample(a.src, a.N, f, (long)(c0 + col) + (long)N1 * n2);
+    {  // rows of nc contiguous samples (lanes walk the column); all loads in flight first
+        constexpr int PER = kGenTile / kGenBlock;
+        float2 v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * kGenBlock;
+            const int n2 = small_div(p, nc), col = p - n2 * nc;
+            v[u] = p < nc * N2 ? frame_sample(a.src, a.N, f, (long)(c0 + col) + (long)N1 * n2)
+                               : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * kGenBlock;
+            const int n2 = small_div(p, nc), col = p - n2 * nc;
+            if (p < nc * N2) b0[col * N2 + n2] = v[u];
+        }
     }
     __syncthreads();
-    gen_engine(b0, N2, nc, a.rlA, a.twA);
+    gen_engine<kGenBlock, kGenTile>(b0, N2, nc, a.rlA, a.twA);
     const float2* X = b0;
     float2* S = a.scratch + f * (long)a.N + (long)c0 * N2;
     for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
@@ -317,12 +344,24 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_b(Gen4Args a) {
     const int nc = min(C, N2 - c0);
     float2* b0 = glds;
     const float2* S = a.scratch + f * (long)a.N;
-    for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
-        const int n1 = small_div(p, nc), col = p - n1 * nc;
-        b0[col * N1 + n1] = S[(long)n1 * N2 + c0 + col];
+    {
+        constexpr int PER = kGenTile / kGenBlock;
+        float2 v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * kGenBlock;
+            const int n1 = small_div(p, nc), col = p - n1 * nc;
+            v[u] = p < nc * N1 ? S[(long)n1 * N2 + c0 + col] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * kGenBlock;
+            const int n1 = small_div(p, nc), col = p - n1 * nc;
+            if (p < nc * N1) b0[col * N1 + n1] = v[u];
+        }
     }
     __syncthreads();
-    gen_engine(b0, N1, nc, a.rlB, a.twB);
+    gen_engine<kGenBlock, kGenTile>(b0, N1, nc, a.rlB, a.twB);
     const float2* X = b0;
     for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
         const int k1 = small_div(p, nc), col = p - k1 * nc;
@@ -476,7 +515,7 @@ void* fftgen_plan_create(int N, int* status) {
     bool ok = true;
     RadixList rl;
     const bool smooth = radices(N, rl);
-    if (smooth && N <= kGenTile) {
+    if (smooth && N <= kGenTileL) {
         p->kind = kTileKind;
         p->rl = rl;
         ok = upload(&p->tw, twiddles(N));
@@ -565,15 +604,27 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         a.src = src;
         a.nframes = fr.nframes;
         a.N = (int)N;
-        a.B = std::max(1, kGenTile / (int)N);
+        const bool wave = N <= kGenTileW, large = N > kGenTile;
+        a.B = large ? 1 : std::max(1, (wave ? kGenTileW : kGenTile) / (int)N);
         a.rl = p->rl;
         a.tw = p->tw;
         a.norm = p->norm;
         a.store_mode = store_mode;
         a.out = out;
         const long blocks = (fr.nframes + a.B - 1) / a.B;
-        hipLaunchKernelGGL(gen_tile_kernel, dim3((unsigned)blocks), dim3(kGenBlock),
-                           (size_t)a.B * N * sizeof(float2), s, a);
+        if (large) {
+            static const bool attr = hipFuncSetAttribute(
+                (const void*)gen_tile_kernel<kGenBlockL, kGenTileL>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, kGenTileL * (int)sizeof(float2)) == hipSuccess;
+            if (!attr) return SDRGPU_ERR_LAUNCH;
+            hipLaunchKernelGGL((gen_tile_kernel<kGenBlockL, kGenTileL>), dim3((unsigned)blocks),
+                               dim3(kGenBlockL), (size_t)N * sizeof(float2), s, a);
+        } else if (wave)
+            hipLaunchKernelGGL((gen_tile_kernel<64, kGenTileW>), dim3((unsigned)blocks), dim3(64),
+                               (size_t)a.B * N * sizeof(float2), s, a);
+        else
+            hipLaunchKernelGGL((gen_tile_kernel<kGenBlock, kGenTile>), dim3((unsigned)blocks),
+                               dim3(kGenBlock), (size_t)a.B * N * sizeof(float2), s, a);
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
     }
