@@ -21,8 +21,9 @@ elif v == "nodb":
     old = "else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);"
     assert old in s; s = s.replace(old, "else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = x.x * a.norm;")
 elif v == "noload":
-    old = "v[u] = (p < L && f < nf) ? frame_sample(a.src, N, f0 + f, n) : make_float2(0.f, 0.f);"
-    assert old in s; s = s.replace(old, "v[u] = make_float2((float)n, (float)f);")
+    old = "gather_tile<PER, BLK>(a.src, N, f0, nf, L, [&](int p) { return a.rl.dn.div(p); }, v);"
+    assert old in s
+    s = s.replace(old, "for (int u = 0; u < PER; ++u) v[u] = make_float2((float)u, (float)threadIdx.x);")
 open(p, 'w').write(s)
 PY
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fft_gen_$v.o
