@@ -69,6 +69,15 @@ struct RadixList {
     FastDiv dn;             // N
 };
 
+// LDS index of tile point i: one float2 of padding per 32, so the stride-R writes of a
+// Stockham pass (R = 8, 16: 16- to 32-way bank conflicts unpadded) spread over the banks
+// (the 16K-point single-frame tile only: at <= 4096 points the extra index arithmetic and
+// the lost workgroup per CU cost more than the conflicts, profiles/r02_fft_anyn.txt)
+template <int TILE>
+__host__ __device__ __forceinline__ int lp(int i) { return TILE > 4096 ? i + (i >> 5) : i; }
+template <int TILE>
+__host__ inline size_t lp_bytes(int points) { return (size_t)lp<TILE>(points) * sizeof(float2) + sizeof(float2); }
+
 // ---- butterflies -----------------------------------------------------------------------
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 __device__ __forceinline__ float2 cfma(float s, float2 a, float2 acc) {
@@ -174,9 +183,9 @@ __device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
         if (g < total) {
             const int f = dq.div(g), j = g - f * Q;
             const int k = j - Ns * dns.div(j);
-            const float2* s = buf + f * N + j;
+            const int s0 = f * N + j;
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[u][r] = s[r * Q];
+            for (int r = 0; r < R; ++r) v[u][r] = buf[lp<TILE>(s0 + r * Q)];
             if (Ns > 1) twiddle_tree<R>(v[u], tw[k * step]);  // W^{r k step} = (W^{k step})^r
             dft_any<R>(v[u], tw, N);
             dsto[u] = f * N + (j - k) * R + k;
@@ -186,9 +195,8 @@ __device__ __forceinline__ void gen_pass(float2* buf, int N, int B, int Ns,
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
         if (dsto[u] >= 0) {
-            float2* d = buf + dsto[u];
 #pragma unroll
-            for (int r = 0; r < R; ++r) d[r * Ns] = v[u][r];
+            for (int r = 0; r < R; ++r) buf[lp<TILE>(dsto[u] + r * Ns)] = v[u][r];
         }
     }
 }
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int p = threadIdx.x + u * BLK;
-            if (p < L) b0[p] = v[u];
+            if (p < L) b0[lp<TILE>(p)] = v[u];
         }
     }
     __syncthreads();
@@ -260,14 +268,14 @@ __global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
             const int f = a.rl.dn.div(p), o = p - f * N;
             int k = o + sh;
             if (k >= N) k -= N;
-            const float2 x = X[f * N + k];
+            const float2 x = X[lp<TILE>(f * N + k)];
             if (a.store_mode == 0) a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
             else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);
         }
     } else {
         for (int p = threadIdx.x; p < nf * N; p += BLK) {
             const int f = a.rl.dn.div(p), k = p - f * N;
-            store_bin(a.out, f0 + f, N, k, X[p], a.store_mode, a.norm);
+            store_bin(a.out, f0 + f, N, k, X[lp<TILE>(p)], a.store_mode, a.norm);
         }
     }
 }
@@ -320,7 +328,7 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
         for (int u = 0; u < PER; ++u) {
             const int p = threadIdx.x + u * kGenBlock;
             const int n2 = small_div(p, nc), col = p - n2 * nc;
-            if (p < nc * N2) b0[col * N2 + n2] = v[u];
+            if (p < nc * N2) b0[lp<kGenTile>(col * N2 + n2)] = v[u];
         }
     }
     __syncthreads();
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_a(Gen4Args a) {
     float2* S = a.scratch + f * (long)a.N + (long)c0 * N2;
     for (int p = threadIdx.x; p < nc * N2; p += kGenBlock) {
         const int col = a.rlA.dn.div(p), k2 = p - col * N2;
-        S[p] = cmul(X[p], a.twN[(c0 + col) * k2]);   // (n1 k2 < N)
+        S[p] = cmul(X[lp<kGenTile>(p)], a.twN[(c0 + col) * k2]);   // (n1 k2 < N)
     }
 }
 
@@ -357,7 +365,7 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_b(Gen4Args a) {
         for (int u = 0; u < PER; ++u) {
             const int p = threadIdx.x + u * kGenBlock;
             const int n1 = small_div(p, nc), col = p - n1 * nc;
-            if (p < nc * N1) b0[col * N1 + n1] = v[u];
+            if (p < nc * N1) b0[lp<kGenTile>(col * N1 + n1)] = v[u];
         }
     }
     __syncthreads();
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(kGenBlock) void gen4_pass_b(Gen4Args a) {
     for (int p = threadIdx.x; p < nc * N1; p += kGenBlock) {
         const int k1 = small_div(p, nc), col = p - k1 * nc;
         const long k = (long)(c0 + col) + (long)N2 * k1;
-        store_bin(a.out, f, a.N, k, X[col * N1 + k1], a.store_mode, a.norm);
+        store_bin(a.out, f, a.N, k, X[lp<kGenTile>(col * N1 + k1)], a.store_mode, a.norm);
     }
 }
 
@@ -424,11 +432,9 @@ bool radices(int n, RadixList& rl) {
         n /= 2;
         ++twos;
     }
-    while (twos >= 4) {
-        rl.R[rl.n++] = 16;
-        twos -= 4;
-    }
-    if (twos) rl.R[rl.n++] = 1 << twos;
+    // odd radices first, the power-of-two radices last: a Stockham pass writes at stride R
+    // while Ns = 1 and contiguously once Ns = N / R, so the 8 / 16 (bank-conflicting at
+    // stride R) go where their writes are contiguous
     for (int p : {3, 5, 7, 11, 13}) {
         while (n % p == 0) {
             if (rl.n >= kMaxPass) return false;
@@ -437,6 +443,11 @@ bool radices(int n, RadixList& rl) {
         }
     }
     if (n != 1) return false;
+    if (twos % 4) rl.R[rl.n++] = 1 << (twos % 4);
+    for (; twos >= 4; twos -= 4) {
+        if (rl.n >= kMaxPass) return false;
+        rl.R[rl.n++] = 16;
+    }
     int N = 1, Ns = 1;
     for (int i = 0; i < rl.n; ++i) N *= rl.R[i];
     for (int i = 0; i < rl.n; ++i) {
@@ -615,16 +626,16 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         if (large) {
             static const bool attr = hipFuncSetAttribute(
                 (const void*)gen_tile_kernel<kGenBlockL, kGenTileL>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, kGenTileL * (int)sizeof(float2)) == hipSuccess;
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp_bytes<kGenTileL>(kGenTileL)) == hipSuccess;
             if (!attr) return SDRGPU_ERR_LAUNCH;
             hipLaunchKernelGGL((gen_tile_kernel<kGenBlockL, kGenTileL>), dim3((unsigned)blocks),
-                               dim3(kGenBlockL), (size_t)N * sizeof(float2), s, a);
+                               dim3(kGenBlockL), lp_bytes<kGenTileL>(N), s, a);
         } else if (wave)
             hipLaunchKernelGGL((gen_tile_kernel<64, kGenTileW>), dim3((unsigned)blocks), dim3(64),
-                               (size_t)a.B * N * sizeof(float2), s, a);
+                               lp_bytes<kGenTileW>(a.B * N), s, a);
         else
             hipLaunchKernelGGL((gen_tile_kernel<kGenBlock, kGenTile>), dim3((unsigned)blocks),
-                               dim3(kGenBlock), (size_t)a.B * N * sizeof(float2), s, a);
+                               dim3(kGenBlock), lp_bytes<kGenTile>(a.B * N), s, a);
         SDRGPU_LAUNCH_CHECK();
         return SDRGPU_OK;
     }
@@ -651,10 +662,10 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
             a.nframes = nf;
             a.out = store_advance(out, f0, N, store_mode);
             hipLaunchKernelGGL(gen4_pass_a, dim3((unsigned)(nf * ta)), dim3(kGenBlock),
-                               (size_t)std::min(CA, p->N1) * p->N2 * sizeof(float2), s, a);
+                               lp_bytes<kGenTile>(std::min(CA, p->N1) * p->N2), s, a);
             SDRGPU_LAUNCH_CHECK();
             hipLaunchKernelGGL(gen4_pass_b, dim3((unsigned)(nf * tb)), dim3(kGenBlock),
-                               (size_t)std::min(CB, p->N2) * p->N1 * sizeof(float2), s, a);
+                               lp_bytes<kGenTile>(std::min(CB, p->N2) * p->N1), s, a);
             SDRGPU_LAUNCH_CHECK();
         }
         return SDRGPU_OK;
