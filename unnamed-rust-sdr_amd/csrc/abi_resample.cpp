@@ -225,6 +225,8 @@ struct sdrgpu_src_state {
             index_inc = kSincSpec[type].inc;
             int bl = 3 * (int)std::lrint((coeff_half_len + 2.0) / index_inc * kSrcMaxRatio + 1);
             if (bl < 4096) bl = 4096;
+            // libsamplerate keeps buffer indices in int; so does the device window
+            if ((long)bl * channels + 1 > (long)(INT32_MAX / 4)) return SDRGPU_SRC_ERR_MALLOC_FAILED;
             b_len = bl * channels + 1;
             if (d_coeffs.ensure(c.size() * sizeof(float)) ||
                 hipMemcpy(d_coeffs.ptr, c.data(), c.size() * sizeof(float),
@@ -414,7 +416,10 @@ struct sdrgpu_src_state {
         const double terminate = 1.0 / src_ratio + 1e-20;
         const bool eoi = d.end_of_input != 0;
         appends.clear();
-        if (int st = sinc_window(in_count + 2L * b_len + 16)) return st;
+        // this call appends at most its input, the lead-in zeros and the end-of-input tail
+        // (2 half + 5 <= b_len); window indices are int
+        if (in_count + 2L * b_len > (long)(INT32_MAX / 2)) return SDRGPU_SRC_ERR_BAD_DATA;
+        if (int st = sinc_window(in_count + (long)b_len + 16)) return st;
         const size_t cap_frames = max_out_frames(d);
         PinnedBytes& hb = desc_host[slot];
         if (hb.ensure(cap_frames * sizeof(SincDesc) + sizeof(SincDesc)))
