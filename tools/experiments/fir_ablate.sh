@@ -31,6 +31,15 @@ assert old in s
 s = s.replace(old, "const float2* src2 = p.dummy;")
 open(p, 'w').write(s)
 PY
+  elif [ $v = prio ]; then  # static s_setprio 1 for the younger half (waves 4-7) of the workgroup
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);"
+assert old in s
+s = s.replace(old, old + "\n    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);")
+open(p, 'w').write(s)
+PY
   elif [ $v = wvdiv ]; then  # wave index left divergent (VGPR cursor math, no SGPR spills)
     python3 - $src <<'PY'
 import sys

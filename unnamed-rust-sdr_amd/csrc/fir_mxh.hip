@@ -221,6 +221,10 @@ void fir_mxh_kernel(MxhParams p) {
     const int lane = threadIdx.x & 63;
     // wave-uniform (readfirstlane), so the tile cursors and channel addressing stay scalar
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the younger half of the workgroup (waves 4-7) loses VALU arbitration to its SIMD partner
+    // on every segment (priority, then age): one static s_setprio 1 for it, no per-segment
+    // flips (configs[1]: 0.5229 -> 0.5189 ms over 3 A/B reps, profiles/r02_fir_prio_ab.txt)
+    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
     const long wave = (long)blockIdx.x * kWaves + wv;
     const long nwaves = (long)gridDim.x * kWaves;
     const int g = lane >> 4, v = lane & 15;
