@@ -40,6 +40,27 @@ assert old in s
 s = s.replace(old, old + "\n    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);")
 open(p, 'w').write(s)
 PY
+  elif [ $v = stplain ]; then  # plain (temporal) output stores instead of non-temporal
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """                    __builtin_nontemporal_store(y0, o4);
+                    __builtin_nontemporal_store(y1, o4 + 1);"""
+assert old in s
+s = s.replace(old, """                    o4[0] = y0;
+                    o4[1] = y1;""")
+open(p, 'w').write(s)
+PY
+  elif [ $v = ldplain ]; then  # plain loads for the streamed tiles instead of non-temporal
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """                        const f32x4 r = __builtin_nontemporal_load(
+                            reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane));"""
+assert old in s
+s = s.replace(old, """                        const f32x4 r = *reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane);""")
+open(p, 'w').write(s)
+PY
   elif [ $v = wvdiv ]; then  # wave index left divergent (VGPR cursor math, no SGPR spills)
     python3 - $src <<'PY'
 import sys
