@@ -70,6 +70,66 @@ assert old in s
 s = s.replace(old, "const int wv = threadIdx.x >> 6;")
 open(p, 'w').write(s)
 PY
+  elif [ $v = nohist ]; then  # history groups not re-staged per window (wrong outputs: cost probe)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);"
+assert old in s
+s = s.replace(old, "                    for (int k = 0; k < NH; ++k) if (scn == 0.f) put(WN + hist_addr(k), hr[k], scn);")
+open(p, 'w').write(s)
+PY
+  elif [ $v = nosplit ]; then  # hi plane only, lo = 0 (wrong precision: split-VALU cost probe)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    lo = pk_rtz(a - lo_f(hi), b - hi_f(hi));"
+assert old in s
+s = s.replace(old, "    lo = 0u;")
+open(p, 'w').write(s)
+PY
+  elif [ $v = nomax ]; then  # fixed window scale (no abs-max / wave reduction: cost probe)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "            return wave_scale(m);"
+assert old in s
+s = s.replace(old, "            return 15;")
+open(p, 'w').write(s)
+PY
+  elif [ $v = early ]; then  # stage all of tile k+1 and issue all of tile k+2's loads BEFORE tile k's MFMAs
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old_a = """            read_frags(fb[0], 0, 0);
+#pragma unroll
+            for (int i = 0; i < CS * NCH; ++i) {"""
+new_a = """#pragma unroll
+            for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
+            if (ld_run) load_hist(hr, ld);
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                put(WN + new_addr(k), nx[k], scn);
+                if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
+                if constexpr (U8) {
+                    nx[k] = __builtin_nontemporal_load(src2u + 64 * k + lane);
+                } else {
+                    const f32x4 r = __builtin_nontemporal_load(
+                        reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane));
+                    nx[k] = make_float4(r[0], r[1], r[2], r[3]);
+                }
+            }
+            read_frags(fb[0], 0, 0);
+#pragma unroll
+            for (int i = 0; i < CS * NCH; ++i) {"""
+assert old_a in s
+s = s.replace(old_a, new_a)
+old_b = """                if (i == 0) {  // window k+1's history (old hr); then tile k+2's, if it opens a run"""
+i0 = s.index(old_b)
+i1 = s.index("            }\n            if (!ld_run) {", i0)
+s = s[:i0] + s[i1:]
+open(p, 'w').write(s)
+PY
   fi
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
