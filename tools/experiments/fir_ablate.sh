@@ -130,6 +130,27 @@ i1 = s.index("            }\n            if (!ld_run) {", i0)
 s = s[:i0] + s[i1:]
 open(p, 'w').write(s)
 PY
+  elif [ $v = wgtime ]; then  # per-workgroup start/end s_memrealtime (100 MHz) into out[0..511]: tail census
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    const int lane = threadIdx.x & 63;"
+assert old in s
+s = s.replace(old, "    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();\n" + old, 1)
+old2 = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
+assert old2 in s
+s = s.replace(old2, """    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* o = reinterpret_cast<unsigned long long*>(p.out) + 2 * blockIdx.x;
+        o[0] = t_start | ((unsigned long long)(xcc & 7) << 56);
+        o[1] = t_end;
+    }
+""" + old2, 1)
+open(p, 'w').write(s)
+PY
   fi
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
