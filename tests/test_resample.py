@@ -255,13 +255,37 @@ def test_src_sinc_bit_exact(sdr, oracle, conv, ratio, ch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ch,ratio", [(100, 48000 * 3.0 / 1.8e6), (64, 2.5), (300, 1 / 200.0)])
+@pytest.mark.parametrize("ch,ratio", [(100, 48000 * 3.0 / 1.8e6), (64, 2.5), (300, 1 / 200.0),
+                                      (1100, 48000 * 3.0 / 1.8e6), (1024, 2.5)])
 def test_src_sinc_wide_frames(sdr, oracle, ch, ratio):
     """Wide-frame sinc kernel (>= 64 channels: LDS-staged coefficients, partial channel
-    tiles, tap chunks beyond 1024 at ratio 1/200) against the oracle, ragged blocks."""
+    tiles, tap chunks beyond 1024 at ratio 1/200, 1024 / 1100 channels) against the oracle,
+    ragged blocks."""
     rng = np.random.default_rng(ch)
-    x = rng.standard_normal((2000 if ratio > 0.01 else 6000, ch)).astype(np.float32)
+    x = rng.standard_normal((2000 if ratio > 0.01 else 6000, ch) if ch < 1000 else (700, ch)).astype(np.float32)
     _run_both(sdr, oracle, FASTEST, ch, ratio, x, rng)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ch", [96, 1030])
+def test_src_sinc_wide_frames_nonfinite(sdr, oracle, ch):
+    """Wide-frame sinc kernel with NaN / +-inf samples in a few channels: the frames whose taps
+    cover them (and only those) go non-finite, exactly as the restatement does."""
+    from sdrgpu import resample
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((3000 if ch < 1000 else 900, ch)).astype(np.float32)
+    x[700, 5] = np.nan
+    x[500, 40] = np.inf
+    x[510, 41] = -np.inf
+    g = resample.SampleRate(FASTEST, ch)
+    o = oracle.SampleRate(FASTEST, ch)
+    ratio = 48000 * 3.0 / 1.8e6
+    gu, ga = g.process(ratio, x, 1 << 14)
+    ou, oa = o.process(ratio, x, 1 << 14)
+    assert gu == ou and ga.shape == oa.shape
+    np.testing.assert_array_equal(ga, oa)  # NaN == NaN here
+    assert np.isnan(ga[:, 5]).any() and np.isfinite(ga[:, 6]).all()
+    assert np.isfinite(ga[:, 4]).all() and not np.isfinite(ga[:, 40]).all()
 
 
 @pytest.mark.gpu
