@@ -491,7 +491,8 @@ struct sdrgpu_src_state {
             hb.pending = true;
             slot ^= 1;
             if (src_sinc_launch(w, ch, static_cast<const SincDesc*>(d_desc.ptr), k,
-                                static_cast<const float*>(d_coeffs.ptr), d_out, stream.cur))
+                                static_cast<const float*>(d_coeffs.ptr), coeff_half_len + 2, d_out,
+                                stream.cur))
                 return SDRGPU_SRC_ERR_BAD_STATE;
         }
         d.input_frames_used = in_used / ch;

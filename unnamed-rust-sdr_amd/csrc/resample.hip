@@ -166,6 +166,137 @@ __global__ __launch_bounds__(kSrcBlock) void src_sinc_kernel(
     }
 }
 
+// Mono / stereo streams (src/main.rs:50 resamples the mono FM audio with SincFastest): one
+// lane per output frame leaves each lane a serial chain of ~481 taps, each waiting on its
+// loads (59 us for a 4096-sample call, 2 workgroups on the whole chip).  The products do not
+// depend on the running sums, only the sums are ordered, so a workgroup takes kSincItems
+// (frame, channel) items: its 256 lanes first compute every tap product of the items in
+// parallel (window span and, when short, the coefficient table staged in LDS) into an f64
+// LDS array, then one lane per item adds its products in the reference order (left taps
+// ascending, right taps descending: the same __dmul_rn / __dadd_rn values and order as the
+// global path, so outputs are bit-identical).  Items whose products do not fit take the
+// sequential path below.
+constexpr int kSincItems = 8;
+constexpr int kProdLds = 8192;   // f64 products per workgroup (64 KiB): 8 items of <= 1024 taps
+constexpr int kWinLds = 4096;    // window floats staged per workgroup (16 KiB)
+constexpr int kCoefLds = 4096;   // coefficient floats staged when the table fits (16 KiB)
+
+template <int CH>
+__global__ __launch_bounds__(kSrcBlock) void src_sinc_lds_kernel(
+    const float* __restrict__ win, const SincDesc* __restrict__ desc, long nframes,
+    const float* __restrict__ coeffs, int coeff_len, float* __restrict__ out) {
+    __shared__ double prod[kProdLds];
+    __shared__ float wl[kWinLds];
+    __shared__ float cl[kCoefLds];
+    __shared__ int pofs[kSincItems + 1];
+    __shared__ SincDesc sd[kSincItems];
+    __shared__ long span_lo, span_hi;
+    constexpr long C = CH;
+    const long total = nframes * C;
+    const long t0 = (long)blockIdx.x * kSincItems;
+    const int ni = (int)(total - t0 < kSincItems ? total - t0 : kSincItems);
+    if (threadIdx.x < 64) {  // wave 0: the items' descriptors (one load per lane, in parallel),
+                             // product offsets (prefix sum) and the window span
+        const int i = threadIdx.x;
+        long lo = 0x7fffffffffffL, hi = -0x7fffffffffffL;
+        int cnt = 0;
+        if (i < ni) {
+            const long t = t0 + i, k = t / CH, ch = t - k * CH;
+            const SincDesc d = desc[k];
+            sd[i] = d;
+            cnt = (d.nl > 0 ? d.nl : 0) + d.nr;
+            if (d.nl > 0) {
+                lo = min(lo, (long)d.dl + ch);
+                hi = max(hi, (long)d.dl + ch + (long)(d.nl - 1) * C);
+            }
+            lo = min(lo, (long)d.dr + ch - (long)(d.nr - 1) * C);
+            hi = max(hi, (long)d.dr + ch);
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < kSincItems; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (i >= o) incl += v;
+        }
+#pragma unroll
+        for (int o = kSincItems / 2; o > 0; o >>= 1) {
+            lo = min(lo, (long)__shfl_xor(lo, o));
+            hi = max(hi, (long)__shfl_xor(hi, o));
+        }
+        if (i < kSincItems) pofs[i + 1] = incl;
+        if (i == 0) {
+            pofs[0] = 0;
+            span_lo = lo;
+            span_hi = hi;
+        }
+    }
+    __syncthreads();
+    const int np = pofs[ni];
+    const long base = span_lo, n = span_hi - span_lo + 1;
+    const bool fits = np <= kProdLds && n > 0 && n <= kWinLds;  // workgroup-uniform
+    if (!fits) {  // sequential path (very long filters / extreme ratios)
+        if (threadIdx.x < ni) {
+            const long t = t0 + threadIdx.x, k = t / CH, ch = t - k * CH;
+            const SincDesc d = desc[k];
+            double left = 0.0, right = 0.0;
+            int fi = d.fil;
+            long x = (long)d.dl + ch;
+            for (int m = 0; m < d.nl; ++m) {
+                left = __dadd_rn(left, __dmul_rn(sinc_icoeff(coeffs, fi), (double)win[x]));
+                fi -= d.inc;
+                x += C;
+            }
+            fi = d.fir;
+            x = (long)d.dr + ch;
+            for (int m = 0; m < d.nr; ++m) {
+                right = __dadd_rn(right, __dmul_rn(sinc_icoeff(coeffs, fi), (double)win[x]));
+                fi -= d.inc;
+                x -= C;
+            }
+            out[t] = (float)__dmul_rn(d.scale, __dadd_rn(left, right));
+        }
+        return;
+    }
+    const bool lds_coef = coeff_len <= kCoefLds;
+    for (int i = threadIdx.x; i < (int)n; i += kSrcBlock) wl[i] = win[base + i];
+    if (lds_coef)
+        for (int i = threadIdx.x; i < coeff_len; i += kSrcBlock) cl[i] = coeffs[i];
+    __syncthreads();
+    const float* cs = lds_coef ? cl : coeffs;
+    // phase 1: every product of the block's items, in parallel
+    for (int g = threadIdx.x; g < np; g += kSrcBlock) {
+        int i = 0;
+        while (i + 1 < ni && pofs[i + 1] <= g) ++i;
+        const long t = t0 + i, k = t / CH, ch = t - k * CH;
+        const SincDesc& d = sd[i];
+        const int m = g - pofs[i], nl = d.nl > 0 ? d.nl : 0;
+        int fi;
+        long x;
+        if (m < nl) {
+            fi = d.fil - m * d.inc;
+            x = (long)d.dl + ch + (long)m * C;
+        } else {
+            fi = d.fir - (m - nl) * d.inc;
+            x = (long)d.dr + ch - (long)(m - nl) * C;
+        }
+        prod[g] = __dmul_rn(sinc_icoeff(cs, fi), (double)wl[x - base]);
+    }
+    __syncthreads();
+    // phase 2: one lane per item sums its products in the reference order
+    if (threadIdx.x < ni) {
+        const int i = threadIdx.x;
+        const long t = t0 + i;
+        const SincDesc& d = sd[i];
+        const int nl = d.nl > 0 ? d.nl : 0, o = pofs[i];
+        double left = 0.0, right = 0.0;
+#pragma unroll 8
+        for (int m = 0; m < nl; ++m) left = __dadd_rn(left, prod[o + m]);
+#pragma unroll 8
+        for (int m = 0; m < d.nr; ++m) right = __dadd_rn(right, prod[o + nl + m]);
+        out[t] = (float)__dmul_rn(d.scale, __dadd_rn(left, right));
+    }
+}
+
 // Wide frames (channels >= 64, a batch of streams sharing one ratio): a workgroup takes one
 // output frame x 256 channels.  The frame's descriptor is uniform, so its interpolated
 // coefficients are computed once per workgroup into LDS (in chunks of kTapChunk taps) and
@@ -216,8 +347,16 @@ __global__ __launch_bounds__(kSrcBlock) void src_sinc_wide_kernel(
 }  // namespace
 
 int src_sinc_launch(const float* win, long channels, const SincDesc* desc, long nframes,
-                    const float* coeffs, float* out, hipStream_t s) {
+                    const float* coeffs, int coeff_len, float* out, hipStream_t s) {
     if (nframes <= 0 || channels <= 0) return SDRGPU_OK;
+    if ((channels == 1 || channels == 2) && (nframes * channels + kSincItems - 1) / kSincItems <= 0x7fffffffL) {
+        const unsigned g = (unsigned)((nframes * channels + kSincItems - 1) / kSincItems);
+        if (channels == 1)
+            src_sinc_lds_kernel<1><<<g, kSrcBlock, 0, s>>>(win, desc, nframes, coeffs, coeff_len, out);
+        else
+            src_sinc_lds_kernel<2><<<g, kSrcBlock, 0, s>>>(win, desc, nframes, coeffs, coeff_len, out);
+        return hipGetLastError() == hipSuccess ? SDRGPU_OK : SDRGPU_ERR_LAUNCH;
+    }
     if (channels >= 64) {
         const int ntiles = (int)((channels + kSrcBlock - 1) / kSrcBlock);
         const long per_xcd = (nframes * ntiles + 7) / 8;

@@ -18,6 +18,6 @@ int src_interp_launch(bool linear, const float* in, long channels, const int* le
                       const double* frac, long nframes, const float* last_value, float* out,
                       hipStream_t s);
 int src_sinc_launch(const float* win, long channels, const SincDesc* desc, long nframes,
-                    const float* coeffs, float* out, hipStream_t s);
+                    const float* coeffs, int coeff_len, float* out, hipStream_t s);
 
 }  // namespace sdrgpu
