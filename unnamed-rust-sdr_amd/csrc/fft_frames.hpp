@@ -137,8 +137,15 @@ __host__ __device__ inline float2* store_advance(float2* out, long frames, long 
                                      frames * store_stride(mode, M) * store_elem_bytes(mode));
 }
 
+// 20 log10 |X| = (10 log10 2) log2(re^2 + im^2): one v_log_f32 (~1 ulp of log2, i.e. < 1e-5 dB
+// across the range below) instead of the library hypotf + log10f (~40 VALU per bin; the
+// 1000-point live spectrum is VALU-bound).  Where re^2 + im^2 would leave the normal f32
+// range (|X| outside ~1e-18 .. 1e18, and exact zeros) the library pair is used.
 __device__ __forceinline__ float db_of(float2 x, float norm) {
-    return 20.0f * log10f(hypotf(x.x * norm, x.y * norm));
+    const float a = x.x * norm, b = x.y * norm;
+    const float m2 = a * a + b * b;
+    if (m2 > 1e-36f && m2 < 1e36f) return 3.01029995663981195f * __builtin_amdgcn_logf(m2);
+    return 20.0f * log10f(hypotf(a, b));
 }
 
 __device__ __forceinline__ void store_bin(float2* __restrict__ out, long f, long M, long k,
