@@ -280,6 +280,91 @@ __global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
     }
 }
 
+// ---- compile-time plans for the reference examples' sizes -------------------------------
+// examples/live.rs frames 1000 points (window(1000 / rate)); with N, the radix order and every
+// stride known at compile time, the engine's index arithmetic (plan-time divisions, the pass
+// loop's radix switch, the butterfly-count guards) folds into constants: the 1000-point live
+// spectrum is VALU-bound (~2,700 VALU instructions per frame in the generic engine).  Same
+// plan, twiddle table, pass order and arithmetic as gen_pass, so the results are identical.
+template <int R, int BLK, int TILE, int N, int B, int NS>
+__device__ __forceinline__ void fixed_pass(float2* buf, const float2* __restrict__ tw) {
+    constexpr int Q = N / R, TOTAL = B * Q, STEP = N / (NS * R);
+    constexpr int NB = (TOTAL + BLK - 1) / BLK;
+    float2 v[NB][R];
+    int dsto[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int g = threadIdx.x + u * BLK;
+        dsto[u] = -1;
+        if ((u + 1) * BLK <= TOTAL || g < TOTAL) {
+            const int f = g / Q, j = g - f * Q;
+            const int k = j % NS;
+            const int s0 = f * N + j;
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[u][r] = buf[lp<TILE>(s0 + r * Q)];
+            if (NS > 1) twiddle_tree<R>(v[u], tw[k * STEP]);
+            dft_any<R>(v[u], tw, N);
+            dsto[u] = f * N + (j - k) * R + k;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        if (dsto[u] >= 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[lp<TILE>(dsto[u] + r * NS)] = v[u][r];
+        }
+    }
+}
+
+template <int BLK, int TILE, int N, int B, int NS, int R, int... REST>
+__device__ __forceinline__ void fixed_engine(float2* buf, const float2* __restrict__ tw) {
+    fixed_pass<R, BLK, TILE, N, B, NS>(buf, tw);
+    __syncthreads();
+    if constexpr (sizeof...(REST) > 0) fixed_engine<BLK, TILE, N, B, NS * R, REST...>(buf, tw);
+}
+
+template <int BLK, int TILE, int N, int... RS>
+__global__ __launch_bounds__(BLK) void gen_fixed_kernel(GenTileArgs a) {
+    extern __shared__ float2 glds[];
+    constexpr int B = TILE / N, L = B * N;
+    float2* b0 = glds;
+    const long f0 = (long)blockIdx.x * B;
+    const int nf = (int)min((long)B, a.nframes - f0);
+    {
+        constexpr int PER = TILE / BLK;
+        float2 v[PER];
+        gather_tile<PER, BLK>(a.src, N, f0, nf, L, [](int p) { return p / N; }, v);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * BLK;
+            if (p < L) b0[lp<TILE>(p)] = v[u];
+        }
+    }
+    __syncthreads();
+    fixed_engine<BLK, TILE, N, B, 1, RS...>(b0, a.tw);
+    const float2* X = b0;
+    if (a.store_mode == 0 || a.store_mode == 3) {
+        constexpr int SH = N - N / 2;
+#pragma unroll
+        for (int u = 0; u < (L + BLK - 1) / BLK; ++u) {
+            const int p = threadIdx.x + u * BLK;
+            const int f = p / N, o = p - f * N;
+            if (p < L && f < nf) {
+                const int k = o + SH < N ? o + SH : o + SH - N;
+                const float2 x = X[lp<TILE>(f * N + k)];
+                if (a.store_mode == 0) a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
+                else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);
+            }
+        }
+    } else {
+        for (int p = threadIdx.x; p < nf * N; p += BLK) {
+            const int f = p / N, k = p - f * N;
+            store_bin(a.out, f0 + f, N, k, X[lp<TILE>(p)], a.store_mode, a.norm);
+        }
+    }
+}
+
 // ---- four-step over two mixed-radix tiles (n = n1 + N1 n2, k = k2 + N2 k1) -------------
 struct Gen4Args {
     FrameSrc src;
@@ -630,7 +715,11 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
             if (!attr) return SDRGPU_ERR_LAUNCH;
             hipLaunchKernelGGL((gen_tile_kernel<kGenBlockL, kGenTileL>), dim3((unsigned)blocks),
                                dim3(kGenBlockL), lp_bytes<kGenTileL>(N), s, a);
-        } else if (wave)
+        } else if (N == 1000 && a.B == 1 && p->rl.n == 4 && p->rl.R[0] == 5 && p->rl.R[1] == 5 &&
+                   p->rl.R[2] == 5 && p->rl.R[3] == 8)  // examples/live.rs: compile-time plan
+            hipLaunchKernelGGL((gen_fixed_kernel<64, kGenTileW, 1000, 5, 5, 5, 8>), dim3((unsigned)blocks),
+                               dim3(64), lp_bytes<kGenTileW>(N), s, a);
+        else if (wave)
             hipLaunchKernelGGL((gen_tile_kernel<64, kGenTileW>), dim3((unsigned)blocks), dim3(64),
                                lp_bytes<kGenTileW>(a.B * N), s, a);
         else
