@@ -281,7 +281,8 @@ __global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
 }
 
 // ---- compile-time plans for the reference examples' sizes -------------------------------
-// examples/live.rs frames 1000 points (window(1000 / rate)); with N, the radix order and every
+// examples/live.rs frames 1000 points (window(1000 / rate)) and examples/fft.rs rffts 14,400
+// (take(0.1) at 144 kHz); with N, the radix order and every
 // stride known at compile time, the engine's index arithmetic (plan-time divisions, the pass
 // loop's radix switch, the butterfly-count guards) folds into constants: the 1000-point live
 // spectrum is VALU-bound (~2,700 VALU instructions per frame in the generic engine).  Same
@@ -708,7 +709,16 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         a.store_mode = store_mode;
         a.out = out;
         const long blocks = (fr.nframes + a.B - 1) / a.B;
-        if (large) {
+        if (large && N == 14400 && p->rl.n == 6 && p->rl.R[0] == 3 && p->rl.R[1] == 3 &&
+            p->rl.R[2] == 5 && p->rl.R[3] == 5 && p->rl.R[4] == 4 && p->rl.R[5] == 16) {
+            // examples/fft.rs: take(0.1) at 144 kHz, compile-time plan
+            static const bool attr = hipFuncSetAttribute(
+                (const void*)gen_fixed_kernel<kGenBlockL, kGenTileL, 14400, 3, 3, 5, 5, 4, 16>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp_bytes<kGenTileL>(kGenTileL)) == hipSuccess;
+            if (!attr) return SDRGPU_ERR_LAUNCH;
+            hipLaunchKernelGGL((gen_fixed_kernel<kGenBlockL, kGenTileL, 14400, 3, 3, 5, 5, 4, 16>),
+                               dim3((unsigned)blocks), dim3(kGenBlockL), lp_bytes<kGenTileL>(N), s, a);
+        } else if (large) {
             static const bool attr = hipFuncSetAttribute(
                 (const void*)gen_tile_kernel<kGenBlockL, kGenTileL>,
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp_bytes<kGenTileL>(kGenTileL)) == hipSuccess;
