@@ -415,6 +415,9 @@ def bench_c5(args):
     assert res["spot_check_max_over_rms"] <= 1e-5, res["spot_check_max_over_rms"]
     if dist is not None and world > sdrgpu.device_count():
         res["rccl"] = "skipped: ranks share a GPU (RCCL needs one device per rank)"
+        res["note"] = ("ranks share a GPU: a functional rehearsal of the sharded path; each rank's "
+                       "event window need not cover the other ranks' kernels, so value is not a "
+                       "throughput result")
     elif dist is not None:
         # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately);
         # uneven channel blocks (nch % world != 0) go through grouped send / recv
