@@ -236,7 +236,9 @@ def test_stft_db_output(sdr, oracle):
 def test_stft_u8_input(sdr, oracle):
     from sdrgpu import _lib
     rng = np.random.default_rng(6)
-    for n, hop in ((4096, 1000), (65536, 32768)):
+    # (1000, 500): examples/live.rs's rtl.listen().window(..).decimate(..) on the compile-time
+    # 1000-point plan; 14400: the other compile-time plan
+    for n, hop in ((4096, 1000), (65536, 32768), (1000, 500), (14400, 7200)):
         iq = rng.integers(0, 256, 2 * (hop * 4 + 5), dtype=np.uint8)
         s = sdr.fft.Stft(n, hop, input_kind=_lib.CU8)
         y = np.concatenate([s.process(iq[:2 * 777]), s.process(iq[2 * 777:])])
