@@ -151,6 +151,17 @@ s = s.replace(old2, """    __syncthreads();
 """ + old2, 1)
 open(p, 'w').write(s)
 PY
+  elif [ $v = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+for old, new in (("constexpr int kWaves = 8;               // two waves per SIMD", "constexpr int kWaves = 4;  // x 2 workgroups per CU"),
+                 ("const long W = (long)kWaves * cus;", "const long W = (long)kWaves * 2 * cus;"),
+                 ("std::min((long)cus, ceil_div(p.units, kWaves))", "std::min(2L * cus, ceil_div(p.units, kWaves))")):
+    assert old in s, old
+    s = s.replace(old, new)
+open(p, 'w').write(s)
+PY
   fi
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
