@@ -196,3 +196,36 @@ def test_pll_examples_frequency_sweep_kat(sdr, oracle):
     delayed = f[idx - 24]
     assert np.abs(out[idx] - delayed).max() < 50.0     # out ~ f (24-sample filter delay)
     assert np.corrcoef(out[idx], f[idx])[0, 1] > 0.9999
+
+
+@pytest.mark.parametrize("design", ["main", "examples"])
+def test_pll_split_chain_helper_waves(sdr, oracle, design):
+    """Output mode 0 on 64-channel-aligned banks with vector rows runs the chain on one wave
+    and the lock / output filters + stores on a second (pll_split_kernel): two workgroups,
+    device buffers with padded rows, a ragged tail (n % 8 != 0, whole steps after the LDS
+    hand-back of the filter states) and a second call continuing the state; bit-exact."""
+    from sdrgpu.device import DeviceBuffer
+    f = sdr.filter
+    rng = np.random.default_rng(31)
+    nch, n1, n2, ld = 128, 12003, 4000, 16008
+    x = fm_channels(rng, nch, n1 + n2)
+    if design == "main":
+        d, op = main_rs_design(sdr), oracle_params(oracle)
+    else:
+        d = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.BiquadD.LowPass(20000.0, 0.7),
+                        f.BiquadD.LowPass(20000.0, 0.7))
+        op = oracle_params(oracle, outf=(1, 20000.0, 0.7))
+    pll = d.design(RATE, nch=nch)
+    xp = np.zeros((nch, ld), np.complex64)
+    outs, lks = [], []
+    for a, b in ((0, n1), (n1, n1 + n2)):
+        xp[:, :b - a] = x[:, a:b]
+        dx = DeviceBuffer.from_numpy(xp)
+        do = DeviceBuffer.empty(nch * ld, np.float32)
+        dl = DeviceBuffer.empty(nch * ld, np.uint8)
+        pll.process_dev(dx.ptr, ld, b - a, do.ptr, dl.ptr, ld)
+        pll.sync()
+        outs.append(do.download().reshape(nch, ld)[:, :b - a])
+        lks.append(dl.download().reshape(nch, ld)[:, :b - a])
+    ref_out, ref_lk = oracle.pll_batch(op, x, nthreads=8)
+    check(np.concatenate(outs, 1), np.concatenate(lks, 1), ref_out, ref_lk, f"split {design}")

@@ -210,6 +210,147 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
     state[ch] = s;
 }
 
+// Output mode 0 with 64-channel-aligned banks and vector rows (configs[3]'s 1024 channels):
+// the lock and output filters are off the loop-carried chain (pll.rs:78-79 read c.re and
+// phasedif, nothing feeds back), yet inside one wave they take issue slots from it -- and a
+// wave alone on its SIMD is issue-bound.  So a 128-lane workgroup runs the chain on wave 0
+// and the two filters, the output select and the stores on wave 1 (another SIMD): wave 0
+// hands (c.re, phasedif) of each 8-sample chunk over through a two-slot LDS ring, one
+// workgroup barrier per chunk.  Every operation is the same as in pll_kernel (bit-identical).
+template <bool U8, int LID, int OID, int KID>
+__global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
+    PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
+    uint8_t* __restrict__ locked, long ld_out, PllChannelState* __restrict__ state) {
+    __shared__ float2 ring[2][kChunk][kPllBlock];
+    __shared__ float fst[8][kPllBlock];  // the helper's filter states, handed back at the end
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const long ch = (long)blockIdx.x * kPllBlock + lane;  // host: nch % 64 == 0
+    PllChannelState s = state[ch];
+    const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;
+    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;
+    auto cvt = [](unsigned w) -> float2 {
+        return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);
+    };
+    float* __restrict__ y = out + ch * ld_out;
+    uint8_t* __restrict__ lk = locked + ch * ld_out;
+    const Bq L = {p.loopc[0], p.loopc[1], p.loopc[2], p.loopc[3], p.loopc[4]};
+    const Bq O = {p.outc[0], p.outc[1], p.outc[2], p.outc[3], p.outc[4]};
+    const Bq K = {p.lockc[0], p.lockc[1], p.lockc[2], p.lockc[3], p.lockc[4]};
+    const bool loop_id = LID == 2 ? p.loop_ident != 0 : LID == 1;
+    const bool out_id = OID == 2 ? p.out_ident != 0 : OID == 1;
+    const bool lock_id = KID == 2 ? p.lock_ident != 0 : KID == 1;
+    constexpr float kTwoPi = 2.0f * 3.14159265358979323846f;
+    // the loop-carried part of Pll::apply (pll.rs:71-76): returns (c.re, phasedif)
+    auto chain = [&](float2 v) -> float2 {
+        const float cjr = s.vr, cji = -s.vi;
+        const float cr = v.x * cjr - v.y * cji;
+        const float ci = v.x * cji + v.y * cjr;
+        float lr = cr, li = ci;
+        if (!loop_id) {
+            float orr = 0.0f, oi = 0.0f;
+            orr += cr * L.b0;      oi += ci * L.b0;
+            orr += s.lx1r * L.b1;  oi += s.lx1i * L.b1;
+            orr += s.lx2r * L.b2;  oi += s.lx2i * L.b2;
+            orr += s.ly1r * L.na1; oi += s.ly1i * L.na1;
+            orr += s.ly2r * L.na2; oi += s.ly2i * L.na2;
+            s.lx2r = s.lx1r; s.lx1r = cr; s.ly2r = s.ly1r; s.ly1r = orr;
+            s.lx2i = s.lx1i; s.lx1i = ci; s.ly2i = s.ly1i; s.ly1i = oi;
+            lr = orr;
+            li = oi;
+        }
+        const float phasedif = sdr_atan2f_bfx(li, lr) * p.gain;
+        float nph = s.nphase + (p.reference + phasedif);
+        nph = nph - truncf(nph);
+        s.nphase = nph;
+        const float phase = kTwoPi * nph;
+        float sn, cs;
+        sdr_sincosf_bf2(phase, &sn, &cs);
+        s.vr = 1.0f * cs;
+        s.vi = 1.0f * sn;
+        return make_float2(cr, phasedif);
+    };
+    // pll.rs:78-84 (output mode 0)
+    auto filters = [&](float2 cp, float& ov, uint8_t& lv) {
+        const float cr = cp.x, phasedif = cp.y;
+        const float lockv = lock_id ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);
+        const float o = out_id ? phasedif * p.rate
+                               : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
+        const bool lockd = lockv > 0.01f;
+        lv = lockd ? 1 : 0;
+        ov = lockd ? o : 0.0f;
+    };
+    using RawT = std::conditional_t<U8, uint4, float4>;
+    constexpr int NR = U8 ? 1 : kChunk / 2;
+    const long nchunks = n / kChunk, nfull = nchunks * kChunk;
+    if (wv == 0) {  // the chain
+        RawT raw[NR];
+        auto ldc = [&](long i) {
+            const RawT* q = reinterpret_cast<const RawT*>(U8 ? (const void*)(xu + i) : (const void*)(xf + i));
+#pragma unroll
+            for (int r = 0; r < NR; ++r) raw[r] = q[r];
+        };
+        auto sample = [&](int k) -> float2 {
+            if constexpr (U8) {
+                const unsigned w = (&raw[0].x)[k >> 1];
+                return cvt((k & 1) ? (w >> 16) : (w & 0xffffu));
+            } else {
+                const float4 r = raw[k >> 1];
+                return (k & 1) ? make_float2(r.z, r.w) : make_float2(r.x, r.y);
+            }
+        };
+        float2 buf[kChunk];
+        if (nchunks > 0) {
+            ldc(0);
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) buf[k] = sample(k);
+        }
+        for (long c = 0; c < nchunks; ++c) {
+            float2 cur[kChunk];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) cur[k] = buf[k];
+            if (c + 1 < nchunks) {
+                ldc((c + 1) * kChunk);
+#pragma unroll
+                for (int k = 0; k < kChunk; ++k) buf[k] = sample(k);
+            }
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) ring[c & 1][k][lane] = chain(cur[k]);
+            __syncthreads();  // chunk c published; the helper is done with chunk c - 1
+        }
+    } else {  // the filters, the output select and the stores
+        for (long c = 0; c < nchunks; ++c) {
+            __syncthreads();
+            float ov[kChunk];
+            uint8_t lv[kChunk];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) filters(ring[c & 1][k][lane], ov[k], lv[k]);
+            const long i = c * kChunk;
+            float4* yo = reinterpret_cast<float4*>(y + i);
+            yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+            yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
+            uint2 pk;
+            pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
+            pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
+            *reinterpret_cast<uint2*>(lk + i) = pk;
+        }
+        fst[0][lane] = s.kx1; fst[1][lane] = s.kx2; fst[2][lane] = s.ky1; fst[3][lane] = s.ky2;
+        fst[4][lane] = s.ox1; fst[5][lane] = s.ox2; fst[6][lane] = s.oy1; fst[7][lane] = s.oy2;
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    // wave 0: the filter states back, the ragged tail (whole steps), the channel state
+    s.kx1 = fst[0][lane]; s.kx2 = fst[1][lane]; s.ky1 = fst[2][lane]; s.ky2 = fst[3][lane];
+    s.ox1 = fst[4][lane]; s.ox2 = fst[5][lane]; s.oy1 = fst[6][lane]; s.oy2 = fst[7][lane];
+    for (long i = nfull; i < n; ++i) {
+        float o;
+        uint8_t l;
+        filters(chain(U8 ? cvt(xu[i]) : xf[i]), o, l);
+        y[i] = o;
+        lk[i] = l;
+    }
+    state[ch] = s;
+}
+
 template <bool U8, int LID, int OID, int KID, int MODE>
 void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                 uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
@@ -218,7 +359,10 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
     const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in * sb) % 16 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (ld_out % 8) == 0 &&
                      (reinterpret_cast<uintptr_t>(locked) & 7) == 0;
-    if (vec)
+    if (vec && MODE == 0 && p.nch % kPllBlock == 0)
+        hipLaunchKernelGGL((pll_split_kernel<U8, LID, OID, KID>), dim3((unsigned)nblk),
+                           dim3(2 * kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
+    else if (vec)
         hipLaunchKernelGGL((pll_kernel<U8, LID, OID, KID, MODE, true>), dim3((unsigned)nblk),
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
     else
