@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
     state[ch] = s;
 }
 
-// Output mode 0 with 64-channel-aligned banks and vector rows (configs[3]'s 1024 channels):
+// Output mode 0 with vector rows (configs[3]'s 1024 channels, main.rs's single stream):
 // the lock and output filters are off the loop-carried chain (pll.rs:78-79 read c.re and
 // phasedif, nothing feeds back), yet inside one wave they take issue slots from it -- and a
 // wave alone on its SIMD is issue-bound.  So a 128-lane workgroup runs the chain on wave 0
@@ -224,7 +224,10 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
     __shared__ float2 ring[2][kChunk][kPllBlock];
     __shared__ float fst[8][kPllBlock];  // the helper's filter states, handed back at the end
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const long ch = (long)blockIdx.x * kPllBlock + lane;  // host: nch % 64 == 0
+    // lanes past the last channel run a copy of the last channel and store nothing (every
+    // lane takes part in the per-chunk barriers)
+    const bool on = (long)blockIdx.x * kPllBlock + lane < p.nch;
+    const long ch = on ? (long)blockIdx.x * kPllBlock + lane : p.nch - 1;
     PllChannelState s = state[ch];
     const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;
     const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;
@@ -324,14 +327,16 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
             uint8_t lv[kChunk];
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) filters(ring[c & 1][k][lane], ov[k], lv[k]);
-            const long i = c * kChunk;
-            float4* yo = reinterpret_cast<float4*>(y + i);
-            yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
-            yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
-            uint2 pk;
-            pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
-            pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
-            *reinterpret_cast<uint2*>(lk + i) = pk;
+            if (on) {
+                const long i = c * kChunk;
+                float4* yo = reinterpret_cast<float4*>(y + i);
+                yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+                yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
+                uint2 pk;
+                pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
+                pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
+                *reinterpret_cast<uint2*>(lk + i) = pk;
+            }
         }
         fst[0][lane] = s.kx1; fst[1][lane] = s.kx2; fst[2][lane] = s.ky1; fst[3][lane] = s.ky2;
         fst[4][lane] = s.ox1; fst[5][lane] = s.ox2; fst[6][lane] = s.oy1; fst[7][lane] = s.oy2;
@@ -341,6 +346,7 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
     // wave 0: the filter states back, the ragged tail (whole steps), the channel state
     s.kx1 = fst[0][lane]; s.kx2 = fst[1][lane]; s.ky1 = fst[2][lane]; s.ky2 = fst[3][lane];
     s.ox1 = fst[4][lane]; s.ox2 = fst[5][lane]; s.oy1 = fst[6][lane]; s.oy2 = fst[7][lane];
+    if (!on) return;
     for (long i = nfull; i < n; ++i) {
         float o;
         uint8_t l;
@@ -359,7 +365,7 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
     const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in * sb) % 16 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (ld_out % 8) == 0 &&
                      (reinterpret_cast<uintptr_t>(locked) & 7) == 0;
-    if (vec && MODE == 0 && p.nch % kPllBlock == 0)
+    if (vec && MODE == 0)
         hipLaunchKernelGGL((pll_split_kernel<U8, LID, OID, KID>), dim3((unsigned)nblk),
                            dim3(2 * kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
     else if (vec)
