@@ -210,18 +210,21 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
     state[ch] = s;
 }
 
-// Output mode 0 with vector rows (configs[3]'s 1024 channels, main.rs's single stream):
+// Output modes 0 and 1 with vector rows (configs[3]'s 1024 channels, main.rs's single
+// stream and its stereo pilot):
 // the lock and output filters are off the loop-carried chain (pll.rs:78-79 read c.re and
 // phasedif, nothing feeds back), yet inside one wave they take issue slots from it -- and a
 // wave alone on its SIMD is issue-bound.  So a 128-lane workgroup runs the chain on wave 0
 // and the two filters, the output select and the stores on wave 1 (another SIMD): wave 0
 // hands (c.re, phasedif) of each 8-sample chunk over through a two-slot LDS ring, one
 // workgroup barrier per chunk.  Every operation is the same as in pll_kernel (bit-identical).
-template <bool U8, int LID, int OID, int KID>
+template <bool U8, int LID, int OID, int KID, int MODE>
 __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
     PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
     uint8_t* __restrict__ locked, long ld_out, PllChannelState* __restrict__ state) {
     __shared__ float2 ring[2][kChunk][kPllBlock];
+    // output mode 1 (the stereo pilot) also needs the input's real part and the new NCO value
+    __shared__ float4 ring1[MODE == 1 ? 2 : 1][kChunk][kPllBlock];
     __shared__ float fst[8][kPllBlock];  // the helper's filter states, handed back at the end
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // lanes past the last channel run a copy of the last channel and store nothing (every
@@ -272,15 +275,24 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
         s.vi = 1.0f * sn;
         return make_float2(cr, phasedif);
     };
-    // pll.rs:78-84 (output mode 0)
-    auto filters = [&](float2 cp, float& ov, uint8_t& lv) {
+    // pll.rs:78-84; output mode 1: src/main.rs:58-66 from (v.x, new value) in w
+    auto filters = [&](float2 cp, float4 w, float& ov, uint8_t& lv) {
         const float cr = cp.x, phasedif = cp.y;
         const float lockv = lock_id ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);
         const float o = out_id ? phasedif * p.rate
                                : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
         const bool lockd = lockv > 0.01f;
         lv = lockd ? 1 : 0;
-        ov = lockd ? o : 0.0f;
+        if constexpr (MODE == 1) {
+            const float vr = w.y, vi = w.z;
+            const float wr = vr * vr - vi * vi;
+            const float wi = vr * vi + vi * vr;
+            const float nrm = wr * wr + wi * wi;
+            const float dre = w.x * wr / nrm;
+            ov = lockd ? dre * 0.5f : 0.0f;
+        } else {
+            ov = lockd ? o : 0.0f;
+        }
     };
     using RawT = std::conditional_t<U8, uint4, float4>;
     constexpr int NR = U8 ? 1 : kChunk / 2;
@@ -317,7 +329,10 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
                 for (int k = 0; k < kChunk; ++k) buf[k] = sample(k);
             }
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) ring[c & 1][k][lane] = chain(cur[k]);
+            for (int k = 0; k < kChunk; ++k) {
+                ring[c & 1][k][lane] = chain(cur[k]);
+                if constexpr (MODE == 1) ring1[c & 1][k][lane] = make_float4(cur[k].x, s.vr, s.vi, 0.0f);
+            }
             __syncthreads();  // chunk c published; the helper is done with chunk c - 1
         }
     } else {  // the filters, the output select and the stores
@@ -326,7 +341,9 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
             float ov[kChunk];
             uint8_t lv[kChunk];
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) filters(ring[c & 1][k][lane], ov[k], lv[k]);
+            for (int k = 0; k < kChunk; ++k)
+                filters(ring[c & 1][k][lane], MODE == 1 ? ring1[MODE == 1 ? (c & 1) : 0][k][lane] : float4{},
+                        ov[k], lv[k]);
             if (on) {
                 const long i = c * kChunk;
                 float4* yo = reinterpret_cast<float4*>(y + i);
@@ -350,7 +367,9 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
     for (long i = nfull; i < n; ++i) {
         float o;
         uint8_t l;
-        filters(chain(U8 ? cvt(xu[i]) : xf[i]), o, l);
+        const float2 v = U8 ? cvt(xu[i]) : xf[i];
+        const float2 cp = chain(v);
+        filters(cp, make_float4(v.x, s.vr, s.vi, 0.0f), o, l);
         y[i] = o;
         lk[i] = l;
     }
@@ -365,8 +384,8 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
     const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in * sb) % 16 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (ld_out % 8) == 0 &&
                      (reinterpret_cast<uintptr_t>(locked) & 7) == 0;
-    if (vec && MODE == 0)
-        hipLaunchKernelGGL((pll_split_kernel<U8, LID, OID, KID>), dim3((unsigned)nblk),
+    if (vec && (MODE == 0 || MODE == 1))
+        hipLaunchKernelGGL((pll_split_kernel<U8, LID, OID, KID, MODE>), dim3((unsigned)nblk),
                            dim3(2 * kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
     else if (vec)
         hipLaunchKernelGGL((pll_kernel<U8, LID, OID, KID, MODE, true>), dim3((unsigned)nblk),
