@@ -272,13 +272,19 @@ SDR_LIBM_FN void sdr_sincosf_bf2(float y, float* sinp, float* cosp) {
     const double x6 = x4 * x2;
     const double cc = SDR_MAD(x4, SDR_C2, c1);
     const float cp0 = (float)SDR_MAD(x6, c2, cc);         /* cos_poly(xr), table[0] */
-    const uint32_t sgn_s = (((n & 3) == 1) | ((n & 3) == 2)) ? 0x80000000u : 0u;
-    const uint32_t sgn_c = (n & 2) ? 0x80000000u : 0u;
+    /* sign[n & 3] of sinf (negative for n & 3 in {1, 2}, i.e. bit 1 of n + 1) and of the
+     * cosine polynomial (n & 2), as bit arithmetic rather than compares and selects */
+    const uint32_t sgn_s = ((uint32_t)(n + 1) & 2u) << 30;
+    const uint32_t sgn_c = ((uint32_t)n & 2u) << 30;
     const float sp = sdr_asfloat(sdr_asuint(sp0) ^ sgn_s);
     const float cp = sdr_asfloat(sdr_asuint(cp0) ^ sgn_c);
-    const int tiny = sdr_abstop12(y) < 0x398; /* |y| < 2^-12: sinf returns y, cosf 1 */
-    *sinp = tiny ? y : ((n & 1) ? cp : sp);
-    *cosp = tiny ? 1.0f : ((n & 1) ? sp : cp);
+    /* glibc returns y / 1.0f for |y| < 2^-12 without the polynomial; here the polynomial's
+     * own result is used: n = 0, xr = y, and sin_poly(y) = y (1 - e) with e < 2^-26, cos_poly
+     * = 1 - y^2/2 > 1 - 2^-25, which round to exactly y and 1.0f -- except sin(-0), where
+     * x7 * s1 = +0 turns the sum into +0: zeros keep their own sign (checked exhaustively
+     * with the rest, tests/libm_check.c) */
+    *sinp = (y == 0.0f) ? y : ((n & 1) ? cp : sp);
+    *cosp = (n & 1) ? sp : cp;
 }
 
 SDR_LIBM_FN void sdr_sincosf_bf(float y, float* sinp, float* cosp) {
@@ -413,8 +419,7 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     const float t = z - pi_lo;
     const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
     const float gen = m == 0 ? z : m == 1 ? r1 : m == 2 ? pi - t : t - pi;
-    /* special cases, reference order (later checks apply only where earlier ones did not) */
-    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
+    /* special cases, reference order (later checks apply only where earlier ones did not) */    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
     const float half = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;                  /* x == 0, y = inf */
     const float infinf = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny
                        : m == 2 ? (float)3.0 * pi_o_4 + tiny : (float)-3.0 * pi_o_4 - tiny;
