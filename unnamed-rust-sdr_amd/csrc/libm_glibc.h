@@ -377,7 +377,9 @@ SDR_LIBM_FN float sdr_atanf_bf(float x) {
      * branch around the whole evaluation (370 vs 396 ns per PLL sample-chain) */
     __asm__ volatile("" : "+v"(rc));
 #endif
-    return ix >= 0x4c000000 ? rhuge : ix < 0x31000000 ? x : rc;
+    /* s_atanf.c returns x itself for |x| < 2^-29: the small-case polynomial gives exactly x
+     * there (x (s1 + s2) < 2^-58 |x|), so no select (atan2f's argument is |y / x| >= +0) */
+    return ix >= 0x4c000000 ? rhuge : rc;
 }
 
 SDR_LIBM_FN float sdr_atan2f_bf(float y, float x) {
@@ -415,7 +417,9 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     /* common path (its value is discarded wherever a special case applies) */
     const float qq = sdr_fdiv(y, x);
     const float za = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
-    const float z = k > 60 ? pi_o_2 + (float)0.5 * pi_lo : ((hx < 0) & (k < -60)) ? 0.0f : za;
+    /* k > 60 (|y / x| > 2^60): e_atan2f.c's pi_o_2 + 0.5 pi_lo rounds to the same float as
+     * atanf's |x| >= 2^25 constant atanhi[3] + atanlo[3], which the common path returns */
+    const float z = ((hx < 0) & (k < -60)) ? 0.0f : za;
     const float t = z - pi_lo;
     const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
     const float gen = m == 0 ? z : m == 1 ? r1 : m == 2 ? pi - t : t - pi;
