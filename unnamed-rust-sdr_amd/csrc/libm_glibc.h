@@ -335,7 +335,28 @@ SDR_LIBM_FN float sdr_fdiv(float a, float b) {
 #endif
 }
 
-SDR_LIBM_FN float sdr_atanf_bf(float x) {
+/* f32 division num / den restricted to atanf's argument reduction below: den in [1.6, 2^25),
+ * num in [-1, 2) and a normal or exactly zero quotient (lanes outside that -- |x| >= 2^25 or
+ * the small case -- discard the quotient through the selects that follow).  There the division needs no operand
+ * scaling, so on the device it is the f32 reciprocal, one Newton step and two corrected
+ * quotients -- the IEEE sequence the compiler emits around v_div_scale / v_div_fmas /
+ * v_div_fixup, without those three.  Eight full-rate f32 ops instead of sdr_fdiv's half-rate
+ * f64 chain; checked bit-exact against IEEE num / den inside sdr_atanf_bf for every
+ * non-negative finite float argument (tools/atanf_check.hip, 2^31 - 2^23 inputs). */
+SDR_LIBM_FN float sdr_fdiv_n(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float y1 = fmaf(fmaf(-b, y0, 1.0f), y0, y0);
+    const float q0 = a * y1;
+    const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
+    return fmaf(fmaf(-b, q1, a), y1, q1);
+#else
+    return a / b;
+#endif
+}
+
+/* ieee_div != 0: the reduction divides with the IEEE operator (the check tool's ground truth) */
+SDR_LIBM_FN float sdr_atanf_core(float x, int ieee_div) {
     /* finite x (sdr_atan2f_bf routes NaN through the reference function) */
     const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
                 atanhi2 = 9.8279368877e-01f, atanhi3 = 1.5707962513e+00f;
@@ -358,7 +379,7 @@ SDR_LIBM_FN float sdr_atanf_bf(float x) {
     const float num2 = ax - (float)1.5, den2 = one + (float)1.5 * ax;
     const float num = c0 ? num0 : c1 ? num1 : c2 ? num2 : -(float)1.0;
     const float den = c0 ? den0 : c1 ? den1 : c2 ? den2 : ax;
-    const float q = sdr_fdiv(num, den);
+    const float q = ieee_div ? num / den : sdr_fdiv_n(num, den);
     const float xr = small ? x : q;
     const float z = xr * xr;
     const float w = z * z;
@@ -381,6 +402,8 @@ SDR_LIBM_FN float sdr_atanf_bf(float x) {
      * there (x (s1 + s2) < 2^-58 |x|), so no select (atan2f's argument is |y / x| >= +0) */
     return ix >= 0x4c000000 ? rhuge : rc;
 }
+
+SDR_LIBM_FN float sdr_atanf_bf(float x) { return sdr_atanf_core(x, 0); }
 
 SDR_LIBM_FN float sdr_atan2f_bf(float y, float x) {
     const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
