@@ -442,10 +442,13 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     const float za = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
     /* k > 60 (|y / x| > 2^60): e_atan2f.c's pi_o_2 + 0.5 pi_lo rounds to the same float as
      * atanf's |x| >= 2^25 constant atanhi[3] + atanlo[3], which the common path returns */
-    const float z = ((hx < 0) & (k < -60)) ? 0.0f : za;
-    const float t = z - pi_lo;
-    const float r1 = sdr_asfloat(sdr_asuint(z) ^ 0x80000000u);
-    const float gen = m == 0 ? z : m == 1 ? r1 : m == 2 ? pi - t : t - pi;
+    /* quadrant (e_atan2f.c's switch on m): x < 0 gives pi - (z - pi_lo), x >= 0 gives z, and
+     * y's sign is copied on -- m == 1's -z and m == 3's (z - pi_lo) - pi are exactly the
+     * negations (round-to-nearest is symmetric, neither is zero, z >= +0).  With x < 0 and
+     * |y / x| < 2^-60 the reference's z = 0 makes the x < 0 value the constant pi - (0 - pi_lo). */
+    const float zneg = (k < -60) ? pi - (0.0f - pi_lo) : pi - (za - pi_lo);
+    const float zq = (hx < 0) ? zneg : za;
+    const float gen = sdr_asfloat((sdr_asuint(zq) & 0x7fffffffu) | ((uint32_t)hy & 0x80000000u));
     /* special cases, reference order (later checks apply only where earlier ones did not) */    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
     const float half = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;                  /* x == 0, y = inf */
     const float infinf = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny
