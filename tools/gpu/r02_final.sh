@@ -3,7 +3,7 @@
 # bench_configs lines, 2-rank rehearsals.  Outputs under gpurun_out/final/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/final6
+O=$R/gpurun_out/${FINAL_DIR:-final6}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
