@@ -113,6 +113,36 @@ def test_rfft_any_size(sdr, oracle, n):
         assert_parity(y[c], ref, what=f"rfft n={n} frame {c}")
 
 
+def test_rfft_14400_packed_batch_and_unaligned(sdr):
+    """examples/fft.rs's 14,400-point rfft runs as a packed 7,200-point complex transform
+    (two frames per workgroup): an odd frame count against NumPy f64, and a 4-byte-offset
+    input (not c64-aligned: the full 14,400-point kernel takes it) agreeing within parity."""
+    from sdrgpu.device import DeviceBuffer
+    n, count = 14400, 65
+    rng = np.random.default_rng(14400)
+    x = rng.standard_normal((count, n)).astype(np.float32)
+    x[3] = 0.0
+    x[4, 17] = 1.0  # impulse: flat spectrum
+    p = sdr.fft.FftPlan(n)
+    y = p.exec_real(x)
+    for c in (0, 3, 4, 31, count - 1):
+        ref = np.fft.fftshift(np.fft.fft(x[c].astype(np.complex128)))[n // 2:] / np.sqrt(n)
+        if c == 3:
+            assert np.all(y[c] == 0)
+        else:
+            assert_parity(y[c], ref, what=f"packed rfft frame {c}")
+    raw = DeviceBuffer.from_numpy(np.concatenate([np.zeros(1, np.float32), x[:5].ravel()]))
+    dy = DeviceBuffer.empty(5 * (n - n // 2), np.complex64)
+    p.exec_real_dev(raw.ptr + 4, dy.ptr, 5)
+    p.sync()
+    yu = dy.download().reshape(5, n - n // 2)
+    for c in range(5):
+        if c == 3:
+            assert np.all(yu[c] == 0)
+        else:
+            assert_parity(yu[c], y[c].astype(np.complex128), what=f"unaligned rfft frame {c}")
+
+
 @pytest.mark.parametrize("n,hop", [(1000, 400), (1000, 1000), (1001, 333), (14400, 7200),
                                    (4099, 2048)])
 def test_stft_any_size_streaming(sdr, oracle, n, hop):

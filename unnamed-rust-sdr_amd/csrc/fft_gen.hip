@@ -45,6 +45,11 @@ constexpr int kGenTile = 4096;   // complex points per LDS buffer
 constexpr int kGenTileW = 1024;  // one-wave tiles (N <= 1024)
 constexpr int kGenTileL = 16384; // one frame per 1024-lane workgroup, <= 128 KiB of LDS
 constexpr int kGenBlockL = 1024;
+#ifndef RFFT_BLK
+#define RFFT_BLK 1024
+#define RFFT_TILE 8192  // one frame per 1024-lane workgroup: 0.18 ms vs 0.25 (two frames), 0.20 (512 lanes)
+#endif
+constexpr int kRfftBlk = RFFT_BLK, kRfftTile = RFFT_TILE;  // packed 14,400-point rfft
 constexpr int kMaxPass = 16;
 
 // division by a plan-time constant d < 2^16 for dividends < 2^16: q = umulhi(n, ceil(2^32/d))
@@ -366,6 +371,44 @@ __global__ __launch_bounds__(BLK) void gen_fixed_kernel(GenTileArgs a) {
     }
 }
 
+// examples/fft.rs's rfft at its size (real 14,400-point frames, bins [0, N/2) of the collated
+// output, fft.rs:30-37) by the half-length packing: z[n] = x[2n] + i x[2n+1] is the real frame
+// read as NH = N/2 complex points, Z = FFT_NH(z) in LDS (the same compile-time engine), then
+// X[k] = (Z[k] + Z*[NH-k]) / 2 - i W_N^k (Z[k] - Z*[NH-k]) / 2 for the kept bins -- half the
+// transform work of the zero-imaginary N-point transform, same 1/sqrt(N) scale.  Parity is
+// the FFT's (1e-5 of RMS against the f64 DFT), not bit-equality with the full transform.
+template <int BLK, int TILE, int NH, int... RS>
+__global__ __launch_bounds__(BLK) void gen_rfft_half_kernel(GenTileArgs a, const float2* __restrict__ twh) {
+    extern __shared__ float2 glds[];
+    constexpr int B = TILE / NH, L = B * NH;
+    float2* b0 = glds;
+    const long f0 = (long)blockIdx.x * B;
+    const int nf = (int)min((long)B, a.nframes - f0);
+    {
+        constexpr int PER = TILE / BLK;
+        float2 v[PER];
+        gather_tile<PER, BLK>(a.src, NH, f0, nf, L, [](int p) { return p / NH; }, v);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int p = threadIdx.x + u * BLK;
+            if (p < L) b0[lp<TILE>(p)] = v[u];
+        }
+    }
+    __syncthreads();
+    fixed_engine<BLK, TILE, NH, B, 1, RS...>(b0, twh);
+    for (int p = threadIdx.x; p < nf * NH; p += BLK) {
+        const int f = p / NH, k = p - f * NH;
+        const float2 z = b0[lp<TILE>(p)];
+        const float2 m = b0[lp<TILE>(f * NH + (k ? NH - k : 0))];
+        const float ex = 0.5f * (z.x + m.x), ey = 0.5f * (z.y - m.y);
+        const float ox = 0.5f * (z.y + m.y), oy = -0.5f * (z.x - m.x);
+        const float2 w = a.tw[k];  // W_N^k, N = 2 NH
+        const float2 x = make_float2(ex + (w.x * ox - w.y * oy), ey + (w.x * oy + w.y * ox));
+        if (a.store_mode == 1) a.out[(f0 + f) * NH + k] = make_float2(x.x * a.norm, x.y * a.norm);
+        else reinterpret_cast<float*>(a.out)[(f0 + f) * NH + k] = db_of(x, a.norm);
+    }
+}
+
 // ---- four-step over two mixed-radix tiles (n = n1 + N1 n2, k = k2 + N2 k1) -------------
 struct Gen4Args {
     FrameSrc src;
@@ -591,6 +634,7 @@ struct GenFftPlan {
     RadixList rl, rlA, rlB;
     int N1 = 0, N2 = 0;
     float2 *tw = nullptr, *twA = nullptr, *twB = nullptr;
+    float2* tw_half = nullptr;  // W_{N/2} for the packed real transform (N = 14400 only)
     int M = 0;
     void* inner = nullptr;  // power-of-two plan of size M (Bluestein)
     float2 *chirp = nullptr, *bhat = nullptr;
@@ -599,7 +643,7 @@ struct GenFftPlan {
 void fftgen_plan_destroy(void* plan) {
     auto* p = static_cast<GenFftPlan*>(plan);
     if (!p) return;
-    for (float2* q : {p->tw, p->twA, p->twB, p->chirp, p->bhat})
+    for (float2* q : {p->tw, p->twA, p->twB, p->tw_half, p->chirp, p->bhat})
         if (q) (void)hipFree(q);
     if (p->inner) fft_plan_destroy(p->inner);
     delete p;
@@ -616,6 +660,10 @@ void* fftgen_plan_create(int N, int* status) {
         p->kind = kTileKind;
         p->rl = rl;
         ok = upload(&p->tw, twiddles(N));
+        RadixList h;
+        if (ok && N == 14400 && radices(N / 2, h) && h.n == 6 && h.R[0] == 3 && h.R[1] == 3 &&
+            h.R[2] == 5 && h.R[3] == 5 && h.R[4] == 2 && h.R[5] == 16)
+            ok = upload(&p->tw_half, twiddles(N / 2));
     } else if (smooth) {
         int d = (int)std::sqrt((double)N);
         while (d > 1 && (N % d || N / d > kGenTile)) --d;
@@ -709,7 +757,21 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
         a.store_mode = store_mode;
         a.out = out;
         const long blocks = (fr.nframes + a.B - 1) / a.B;
-        if (large && N == 14400 && p->rl.n == 6 && p->rl.R[0] == 3 && p->rl.R[1] == 3 &&
+        if (p->tw_half && (store_mode == 1 || store_mode == 4) && src.mode == 2 &&
+            ((uintptr_t)src.in_real & 7) == 0) {
+            // examples/fft.rs's rfft: real frames as 7,200 complex points, packed transform
+            static const bool attr = hipFuncSetAttribute(
+                (const void*)gen_rfft_half_kernel<kRfftBlk, kRfftTile, 7200, 3, 3, 5, 5, 2, 16>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lp_bytes<kRfftTile>(kRfftTile)) == hipSuccess;
+            if (!attr) return SDRGPU_ERR_LAUNCH;
+            GenTileArgs h = a;
+            h.src.mode = 0;
+            h.src.in = reinterpret_cast<const float2*>(src.in_real);
+            constexpr int B2 = kRfftTile / 7200;
+            hipLaunchKernelGGL((gen_rfft_half_kernel<kRfftBlk, kRfftTile, 7200, 3, 3, 5, 5, 2, 16>),
+                               dim3((unsigned)((fr.nframes + B2 - 1) / B2)), dim3(kRfftBlk),
+                               lp_bytes<kRfftTile>(B2 * 7200), s, h, (const float2*)p->tw_half);
+        } else if (large && N == 14400 && p->rl.n == 6 && p->rl.R[0] == 3 && p->rl.R[1] == 3 &&
             p->rl.R[2] == 5 && p->rl.R[3] == 5 && p->rl.R[4] == 4 && p->rl.R[5] == 16) {
             // examples/fft.rs: take(0.1) at 144 kHz, compile-time plan
             static const bool attr = hipFuncSetAttribute(
