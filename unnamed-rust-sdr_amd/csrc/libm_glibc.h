@@ -435,19 +435,18 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)sdr_asuint(x), ix = hx & 0x7fffffff;
     const int32_t hy = (int32_t)sdr_asuint(y), iy = hy & 0x7fffffff;
-    const int32_t k = (iy - ix) >> 23;
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
     /* common path (its value is discarded wherever a special case applies) */
     const float qq = sdr_fdiv(y, x);
     const float za = sdr_atanf_bf(sdr_asfloat(sdr_asuint(qq) & 0x7fffffffu));
-    /* k > 60 (|y / x| > 2^60): e_atan2f.c's pi_o_2 + 0.5 pi_lo rounds to the same float as
+    /* k = (iy - ix) >> 23 > 60 (|y / x| > 2^60): e_atan2f.c's pi_o_2 + 0.5 pi_lo rounds to the same float as
      * atanf's |x| >= 2^25 constant atanhi[3] + atanlo[3], which the common path returns */
     /* quadrant (e_atan2f.c's switch on m): x < 0 gives pi - (z - pi_lo), x >= 0 gives z, and
      * y's sign is copied on -- m == 1's -z and m == 3's (z - pi_lo) - pi are exactly the
-     * negations (round-to-nearest is symmetric, neither is zero, z >= +0).  With x < 0 and
-     * |y / x| < 2^-60 the reference's z = 0 makes the x < 0 value the constant pi - (0 - pi_lo). */
-    const float zneg = (k < -60) ? pi - (0.0f - pi_lo) : pi - (za - pi_lo);
-    const float zq = (hx < 0) ? zneg : za;
+     * negations (round-to-nearest is symmetric, neither is zero, z >= +0).  The reference's
+     * z = 0 for x < 0 and |y / x| < 2^-60 needs no select either: there za < 2^-59 is below
+     * half an ulp of pi_lo (2^-48), so za - pi_lo rounds to exactly 0 - pi_lo. */
+    const float zq = (hx < 0) ? pi - (za - pi_lo) : za;
     const float gen = sdr_asfloat((sdr_asuint(zq) & 0x7fffffffu) | ((uint32_t)hy & 0x80000000u));
     /* special cases, reference order (later checks apply only where earlier ones did not) */    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
     const float half = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;                  /* x == 0, y = inf */
