@@ -50,6 +50,11 @@ constexpr int kGenBlockL = 1024;
 #define RFFT_TILE 8192  // one frame per 1024-lane workgroup: 0.18 ms vs 0.25 (two frames), 0.20 (512 lanes)
 #endif
 constexpr int kRfftBlk = RFFT_BLK, kRfftTile = RFFT_TILE;  // packed 14,400-point rfft
+#ifndef LIVE_BLK
+#define LIVE_BLK 256  // 4 waves over 2 frames: 0.42 ms vs 0.46-0.47 (one wave per frame), 0.48 (128 lanes)
+#define LIVE_TILE 2048
+#endif
+constexpr int kLiveBlk = LIVE_BLK, kLiveTile = LIVE_TILE;  // 1000-point live spectrum
 constexpr int kMaxPass = 16;
 
 // division by a plan-time constant d < 2^16 for dividends < 2^16: q = umulhi(n, ceil(2^32/d))
@@ -789,8 +794,9 @@ int fftgen_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, 
                                dim3(kGenBlockL), lp_bytes<kGenTileL>(N), s, a);
         } else if (N == 1000 && a.B == 1 && p->rl.n == 4 && p->rl.R[0] == 5 && p->rl.R[1] == 5 &&
                    p->rl.R[2] == 5 && p->rl.R[3] == 8)  // examples/live.rs: compile-time plan
-            hipLaunchKernelGGL((gen_fixed_kernel<64, kGenTileW, 1000, 5, 5, 5, 8>), dim3((unsigned)blocks),
-                               dim3(64), lp_bytes<kGenTileW>(N), s, a);
+            hipLaunchKernelGGL((gen_fixed_kernel<kLiveBlk, kLiveTile, 1000, 5, 5, 5, 8>),
+                               dim3((unsigned)((fr.nframes + kLiveTile / 1000 - 1) / (kLiveTile / 1000))),
+                               dim3(kLiveBlk), lp_bytes<kLiveTile>(kLiveTile / 1000 * 1000), s, a);
         else if (wave)
             hipLaunchKernelGGL((gen_tile_kernel<64, kGenTileW>), dim3((unsigned)blocks), dim3(64),
                                lp_bytes<kGenTileW>(a.B * N), s, a);
