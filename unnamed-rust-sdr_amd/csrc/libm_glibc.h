@@ -456,7 +456,8 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
     float r = gen;
 #if defined(__HIP_DEVICE_COMPILE__)
     /* a wave skips the special-case selects when none of its lanes needs them */
-    const int spec = (iy >= 0x7f800000) | (ix >= 0x7f800000) | (ix == 0) | (iy == 0);
+    /* NaN, +-inf or +-0 in either operand: one class test each (mask 0x267) */
+    const int spec = __builtin_amdgcn_classf(x, 0x267) | __builtin_amdgcn_classf(y, 0x267);
     if (!__builtin_amdgcn_ballot_w64(spec)) return r;
 #endif
     r = (iy == 0x7f800000) ? half : r;
