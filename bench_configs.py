@@ -155,9 +155,24 @@ def bench_c3(args):
         assert st.process_dev(x.ptr, n, y.ptr, nf) == nf
 
     wall, ms = time_events(step, st.stream(), args.steps, args.warmup, lambda: (st.sync(), synchronize()))
+    # spot check of the timed outputs (the last step's): frames at the first scratch-batch
+    # boundaries (both streams of the multi-batch schedule) and the last frame, each against
+    # the oracle FFT of its own span of the tiled input pattern
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pat = cplx_pattern(min(n, 1 << 22), 3)
+    worst = 0.0
+    for j in (0, 255, 256, nf - 1):
+        g = np.arange((j + 1) * hop - N, (j + 1) * hop)
+        span = np.where(g >= 0, pat[np.maximum(g, 0) % pat.size], 0).astype(np.complex64)
+        ref = pyoracle.fft_frame(span).astype(np.complex128)
+        got = y.download(N, offset_bytes=8 * N * j)
+        worst = max(worst, float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2))))
+    assert worst <= 1e-5, worst
     res = {"config": "c3: 64k-point STFT, 50% overlap, fftshift + 1/sqrt(N), 2^28 c64 samples",
            "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
-           "frames": nf, "roofline": roof(24, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
+           "frames": nf, "roofline": roof(24, n, ms), "wall_ms_per_step": round(wall * 1e3, 3),
+           "spot_check_max_over_rms": worst}
     if not args.no_cpu_baseline:
         xf = cplx_pattern(N, 7)
         t0, done = time.perf_counter(), 0

@@ -294,6 +294,17 @@ int sdrgpu_pll_reset(sdrgpu_pll* h);
 int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out);
 void sdrgpu_pll_destroy(sdrgpu_pll* h);
 
+/* Diagnostics (test-only, no reference counterpart): evaluates on `device` the libm
+ * restatements the PLL kernels inline for Pll::apply's arg() and from_polar (pll.rs:72-76;
+ * num-complex calls f32::atan2 / sin / cos, i.e. glibc atan2f / sinf / cosf on x86-64 Linux),
+ * so their special-operand paths can be compared bit for bit with glibc.  HOST pointers,
+ * synchronous.  SDRGPU_DEBUG_ATAN2F: out0[i] = atan2f(a[i], b[i]) (y = a, x = b);
+ * SDRGPU_DEBUG_SINCOSF: out0[i] = sinf(a[i]), out1[i] = cosf(a[i]) (b unused), valid for
+ * |a| < 120 (the PLL's phase argument is 2*pi*nphase, |nphase| < 1). */
+enum sdrgpu_debug_fn { SDRGPU_DEBUG_ATAN2F = 0, SDRGPU_DEBUG_SINCOSF = 1 };
+int sdrgpu_debug_libm(int device, int fn, const float* a, const float* b, float* out0,
+                      float* out1, size_t n);
+
 /* Batched biquad: nch independent Biquad<C, f32> filters (C = F32 or C64) designed by
  * BiquadD::design(rate) (src/filter/biquad.rs:73-155; SDRGPU_BQ_IDENTITY = filter::Identity,
  * src/filter/simple.rs:3-19), applied as Signal::filter (src/signal/mod.rs:42-48) with

@@ -539,6 +539,17 @@ size_t oracle_freq_sweep(float rate, float df, int warmup, float start, float en
 }
 
 /* RtlTcpSignal::next (rtltcp.rs:156-164): (v - 128) / 128 */
+void oracle_libm(int fn, const float* a, const float* b, float* out0, float* out1, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        if (fn == 0) {
+            out0[i] = atan2f(a[i], b[i]);
+        } else {
+            out0[i] = sinf(a[i]);
+            out1[i] = cosf(a[i]);
+        }
+    }
+}
+
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
     for (size_t i = 0; i < 2 * n; ++i) out[i] = ((float)in[i] - 128.0f) / 128.0f;
 }

@@ -125,6 +125,11 @@ size_t oracle_freq_sweep(float rate, float df, int warmup, float start, float en
 /* rtl_tcp u8 IQ -> f32 (src/rtltcp.rs:156-164) */
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out);
 
+/* glibc atan2f (fn 0: out0 = atan2f(a, b)) or sinf / cosf (fn 1: out0 = sinf(a), out1 =
+ * cosf(a)) -- what num-complex's arg() / from_polar call through Rust std in Pll::apply
+ * (src/filter/pll.rs:72-76); the reference for sdrgpu_debug_libm. */
+void oracle_libm(int fn, const float* a, const float* b, float* out0, float* out1, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,7 @@ def lib():
         L.oracle_freq_sweep.argtypes = [c_float, c_float, c_int, c_float, c_float, c_size_t,
                                         c_void_p, c_void_p]
         L.oracle_u8_to_c64.argtypes = [c_void_p, c_size_t, c_void_p]
+        L.oracle_libm.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]
         L.oracle_src_new.restype = c_void_p
         L.oracle_src_new.argtypes = [c_int, c_int, POINTER(c_int)]
         L.oracle_src_delete.argtypes = [c_void_p]
@@ -207,6 +208,23 @@ def u8_to_c64(iq_u8):
     out = np.empty(iq_u8.size // 2, np.complex64)
     lib().oracle_u8_to_c64(iq_u8.ctypes.data, out.size, out.ctypes.data)
     return out
+
+
+def atan2f(y, x):
+    """glibc atan2f elementwise (f32)."""
+    y = np.ascontiguousarray(y, np.float32)
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(y)
+    lib().oracle_libm(0, y.ctypes.data, x.ctypes.data, out.ctypes.data, None, y.size)
+    return out
+
+
+def sincosf(a):
+    """glibc (sinf(a), cosf(a)) elementwise (f32)."""
+    a = np.ascontiguousarray(a, np.float32)
+    s, c = np.empty_like(a), np.empty_like(a)
+    lib().oracle_libm(1, a.ctypes.data, None, s.ctypes.data, c.ctypes.data, a.size)
+    return s, c
 
 
 def sinc_table(converter):

@@ -223,6 +223,65 @@ def test_stft_c3_shape_device(sdr, oracle):
         assert_parity(y[j], ref, what=f"frame {j}")
 
 
+C3_FRAMES = 700   # > 2 x 256: three scratch batches over both streams (fft.hip launch loop)
+C3_CHECK = (0, 1, 255, 256, 257, 511, 512, 513, C3_FRAMES - 2, C3_FRAMES - 1)
+
+
+def _c3_frame_span(x, j, n, hop):
+    """Stream samples of STFT frame j: [(j+1)hop - n, (j+1)hop), zeros before 0
+    (Window zero prefill, src/signal/adapters/mod.rs:277-299)."""
+    beg = (j + 1) * hop - n
+    if beg >= 0:
+        return x[beg:beg + n]
+    return np.concatenate([np.zeros(-beg, x.dtype), x[:beg + n]])
+
+
+@pytest.mark.parametrize("mode", ["c64", "db", "u8"])
+def test_stft_c3_multibatch_schedule(sdr, oracle, mode):
+    """configs[2] exactly as bench_configs.py times it: Stft(65536, 32768).process_dev over
+    700 frames in ONE call, so the 64K four-step runs its two-stream multi-batch schedule
+    (batches of 256 frames alternating between the caller's stream and the plan's aux stream,
+    each with its own half of the scratch slab, joined by events).  Frames at every batch
+    boundary, both streams and the tail are checked against the oracle FFT of the frame's own
+    span (fft.rs:3-28 + Window/Decimate framing), for the c64 store, the fused dB store
+    (complexseries.rs:90-92) and rtl_tcp u8 input (rtltcp.rs:156-164)."""
+    from sdrgpu import _lib
+    from sdrgpu.device import DeviceBuffer
+    n, hop = 65536, 32768
+    total = hop * C3_FRAMES
+    rng = np.random.default_rng(700)
+    if mode == "u8":
+        iq = rng.integers(0, 256, 2 * total, dtype=np.uint8)
+        x = oracle.u8_to_c64(iq)
+        s = sdr.fft.Stft(n, hop, input_kind=_lib.CU8)
+        dx = DeviceBuffer.from_numpy(iq)
+    else:
+        x = cplx(rng, total)
+        s = sdr.fft.Stft(n, hop, output="db" if mode == "db" else "complex")
+        dx = DeviceBuffer.from_numpy(x)
+    nf = s.output_len(total)
+    assert nf == C3_FRAMES
+    obytes = 4 if mode == "db" else 8
+    dy = DeviceBuffer.empty(nf * n * obytes // 8 + 1)
+    assert s.process_dev(dx.ptr, total, dy.ptr, nf) == nf
+    s.sync()
+    for j in C3_CHECK:
+        ref = oracle.fft_frame(_c3_frame_span(x, j, n, hop))
+        if mode == "db":
+            y = dy.download(n, dtype=np.float32, offset_bytes=4 * n * j)
+            _check_db(y, ref, f"c3 db frame {j}")
+        else:
+            y = dy.download(n, offset_bytes=8 * n * j)
+            assert_parity(y, ref, what=f"c3 {mode} frame {j}")
+    # the stream state after the call: the next call's first frame continues the stream
+    if mode == "c64":
+        extra = cplx(rng, hop)
+        y2 = s.process(extra)
+        ref = oracle.fft_frame(np.concatenate([x[-(n - hop):], extra]))
+        assert y2.shape == (1, n)
+        assert_parity(y2[0], ref, what="c3 next-call frame")
+
+
 def _check_db(y_db, ref_c, what):
     """dB output vs the oracle's complex bins: the magnitudes 10^(dB/20) within the FIR/FFT
     parity bound (1e-5 of RMS), and 20 log10 |X| (src/plot/complexseries.rs:90-92)

@@ -229,3 +229,78 @@ def test_pll_split_chain_helper_waves(sdr, oracle, design):
         lks.append(dl.download().reshape(nch, ld)[:, :b - a])
     ref_out, ref_lk = oracle.pll_batch(op, x, nthreads=8)
     check(np.concatenate(outs, 1), np.concatenate(lks, 1), ref_out, ref_lk, f"split {design}")
+
+
+def special_operand_channels(rng, n):
+    """One pathology per channel (so a NaN in one does not hide the others), each run through
+    the loop long enough for the loop filter's output -- atan2f's operands, pll.rs:72 -- to
+    reach it: exact zeros, subnormals, +-inf, NaN, huge / tiny magnitudes and ratios, signed
+    zeros, exact +-1 (x == 1 in e_atan2f.c)."""
+    base = fm_channels(rng, 1, n)[0]
+    chans, names = [], []
+
+    def add(name, x):
+        names.append(name)
+        chans.append(np.asarray(x, np.complex64))
+
+    add("control", base)
+    z = base.copy()
+    z[1000:4000] = 0                     # loop biquad decays through subnormals to exact 0
+    add("zero burst", z)
+    add("all zeros", np.zeros(n, np.complex64))
+    nz = np.full(n, complex(-0.0, -0.0), np.complex64)
+    add("negative zeros", nz)
+    add("subnormal 1e-39", base * np.float32(1e-39))
+    add("subnormal 1e-44", base * np.float32(1e-44))
+    sb = base.copy()
+    sb[2000:2600] *= np.float32(1e-41)   # a subnormal burst inside a locked stream
+    add("subnormal burst", sb)
+    for name, pos, val in (("+inf re", 2000, complex(np.inf, 0)),
+                           ("-inf im", 2000, complex(0, -np.inf)),
+                           ("nan", 2000, complex(np.nan, 1.0))):
+        x = base.copy()
+        x[pos] = val
+        add(name, x)
+    add("huge 1e30", base * np.float32(1e30))
+    with np.errstate(over="ignore"):
+        add("overflow 3e38", base * np.float32(3e38))
+    add("tiny 1e-30", base * np.float32(1e-30))
+    add("re huge / im tiny",
+        (base.real * np.float32(1e30)) + 1j * (base.imag * np.float32(1e-30)))
+    add("re tiny / im huge",
+        (base.real * np.float32(1e-30)) + 1j * (base.imag * np.float32(1e30)))
+    pm = np.where(rng.random(n) < 0.5, 1.0, -1.0).astype(np.float32)
+    add("exact +-1 real", pm.astype(np.complex64))
+    add("exact 1", np.ones(n, np.complex64))
+    return np.stack(chans), names
+
+
+def test_pll_special_operands_bit_exact(sdr, oracle):
+    """Pll::apply (src/filter/pll.rs:70-85) fed the operands that reach atan2f's special-case
+    path (the branch-free selects and their wave ballot, csrc/libm_glibc.h) and the subnormal
+    / overflow ranges of the loop filter: outputs and lock flags equal the oracle's bit for
+    bit (NaN-aware: NaN where the oracle has NaN), on both kernel forms (the split
+    chain/helper kernel on 16-B aligned rows, the single-wave kernel on an odd row pitch)."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(77)
+    n = 6000
+    x, names = special_operand_channels(rng, n)
+    nch = x.shape[0]
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=8)
+    for ld in (n, n + 1):
+        pll = main_rs_design(sdr).design(RATE, nch=nch)
+        xp = np.zeros((nch, ld), np.complex64)
+        xp[:, :n] = x
+        dx = DeviceBuffer.from_numpy(xp)
+        do = DeviceBuffer.empty(nch * ld, np.float32)
+        dl = DeviceBuffer.empty(nch * ld, np.uint8)
+        pll.process_dev(dx.ptr, ld, n, do.ptr, dl.ptr, ld)
+        pll.sync()
+        out = do.download().reshape(nch, ld)[:, :n]
+        lk = dl.download().reshape(nch, ld)[:, :n]
+        for c, name in enumerate(names):
+            assert np.array_equal(lk[c], ref_lk[c]), f"ld={ld} {name}: lock flags differ"
+            g, r = out[c].view(np.uint32), ref_out[c].view(np.uint32)
+            bad = (g != r) & ~(np.isnan(out[c]) & np.isnan(ref_out[c]))
+            assert not bad.any(), (f"ld={ld} {name}: {bad.sum()} outputs differ, first at "
+                                   f"{np.flatnonzero(bad)[0]}")

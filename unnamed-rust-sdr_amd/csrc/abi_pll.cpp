@@ -257,6 +257,37 @@ int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_debug_libm(int device, int fn, const float* a, const float* b, float* out0,
+                      float* out1, size_t n) {
+    if ((fn != SDRGPU_DEBUG_ATAN2F && fn != SDRGPU_DEBUG_SINCOSF) || (n && (!a || !out0)) ||
+        (n && fn == SDRGPU_DEBUG_ATAN2F && !b) || (n && fn == SDRGPU_DEBUG_SINCOSF && !out1))
+        return SDRGPU_ERR_INVALID;
+    if (int st = check_device(device)) return st;
+    if (n == 0) return SDRGPU_OK;
+    DeviceGuard g(device);
+    DevBuf da, db, d0, d1;
+    const size_t bytes = n * sizeof(float);
+    int st = da.ensure(bytes);
+    if (!st) st = d0.ensure(bytes);
+    if (!st && fn == SDRGPU_DEBUG_ATAN2F) st = db.ensure(bytes);
+    if (!st && fn == SDRGPU_DEBUG_SINCOSF) st = d1.ensure(bytes);
+    if (!st && hipMemcpy(da.ptr, a, bytes, hipMemcpyHostToDevice) != hipSuccess) st = SDRGPU_ERR_DEVICE;
+    if (!st && db.ptr && hipMemcpy(db.ptr, b, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        st = SDRGPU_ERR_DEVICE;
+    if (!st)
+        st = libm_debug_launch(fn, (const float*)da.ptr, (const float*)db.ptr, (float*)d0.ptr,
+                               (float*)d1.ptr, (long)n, nullptr);
+    if (!st && hipDeviceSynchronize() != hipSuccess) st = SDRGPU_ERR_DEVICE;
+    if (!st && hipMemcpy(out0, d0.ptr, bytes, hipMemcpyDeviceToHost) != hipSuccess) st = SDRGPU_ERR_DEVICE;
+    if (!st && d1.ptr && hipMemcpy(out1, d1.ptr, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        st = SDRGPU_ERR_DEVICE;
+    da.release();
+    db.release();
+    d0.release();
+    d1.release();
+    return st;
+}
+
 void sdrgpu_pll_destroy(sdrgpu_pll* h) {
     if (!h) return;
     h->free_all();

@@ -591,13 +591,11 @@ size_t fft_scratch_frames(void* plan) {
     auto* p = static_cast<FftPlanDev*>(plan);
     const size_t per = frame_scratch_bytes(p);
     if (per == 0) return 0;
-    // scratch slab of ~256 MiB (the MALL size): 512 workgroups per pass, 32 launches per 2^28
+    // scratch slab of 256 MiB (the MALL size): 512 workgroups per pass, 32 launches per 2^28
     // samples; measured 2.79 ms vs 2.92 (128 MiB), 3.08 (64 MiB), 3.23 (512 MiB)
-    static const size_t mib = [] {
-        const char* e = getenv("SDRGPU_FFT_SLAB_MIB");
-        return (size_t)(e ? atoi(e) : 256);
-    }();
-    return std::max<size_t>(1, (mib << 20) / per);
+    // (profiles/r01_fft64k_experiments.txt)
+    constexpr size_t kSlabBytes = (size_t)256 << 20;
+    return std::max<size_t>(1, kSlabBytes / per);
 }
 
 int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, float2* scratch,
@@ -652,24 +650,12 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
         }
     }
     if (!scratch || scratch_frames == 0) return SDRGPU_ERR_UNSUPPORTED;
-    static const bool use64 = [] {
-        const char* e = getenv("SDRGPU_FFT64K");
-        return !e || atoi(e) != 0;
-    }();
-    if (p->M == 65536 && use64) {
-        static const int cb = [] {
-            const char* e = getenv("SDRGPU_FFT64K_CB");
-            return e && atoi(e) == 64 ? 64 : 32;
-        }();
-        static const bool nt = [] {
-            const char* e = getenv("SDRGPU_FFT64K_NT");
-            return !e || atoi(e) != 0;
-        }();
-        static const int nstreams = [] {
-            const char* e = getenv("SDRGPU_FFT64K_STREAMS");  // default 2 (2.63-2.70 vs 2.77-2.79 ms)
-            return e && atoi(e) == 1 ? 1 : 2;
-        }();
-        const bool two = nstreams == 2 && scratch_frames >= 2 && fr.nframes > (long)scratch_frames / 2;
+    if (p->M == 65536) {
+        // 32 columns per workgroup (CB = 64: 3.36 vs 2.94 ms), non-temporal stream loads and
+        // stores (2.92 vs 3.01 ms), two streams once there is more than half a slab of frames
+        // (2.63-2.70 vs 2.77-2.79 ms): profiles/r01_fft64k_experiments.txt
+        constexpr int cb = 32;
+        const bool two = scratch_frames >= 2 && fr.nframes > (long)scratch_frames / 2;
         if (two && !p->aux) {
             if (hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -700,23 +686,9 @@ int fft_launch(void* plan, const FftFrames& fr, float2* out, int store_mode, flo
             a.nframes = nf;
             a.out = store_advance(out, f0, p->M, store_mode);
             const dim3 g((unsigned)(nf * (256 / cb))), b(16 * cb);
-            if (cb == 64 && nt) {
-                hipLaunchKernelGGL((fft64k_pass_a<64, true>), g, b, 0, st, a);
-                SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<64, true>), g, b, 0, st, a);
-            } else if (cb == 64) {
-                hipLaunchKernelGGL((fft64k_pass_a<64, false>), g, b, 0, st, a);
-                SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<64, false>), g, b, 0, st, a);
-            } else if (nt) {
-                hipLaunchKernelGGL((fft64k_pass_a<32, true>), g, b, 0, st, a);
-                SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<32, true>), g, b, 0, st, a);
-            } else {
-                hipLaunchKernelGGL((fft64k_pass_a<32, false>), g, b, 0, st, a);
-                SDRGPU_LAUNCH_CHECK();
-                hipLaunchKernelGGL((fft64k_pass_b<32, false>), g, b, 0, st, a);
-            }
+            hipLaunchKernelGGL((fft64k_pass_a<cb, true>), g, b, 0, st, a);
+            SDRGPU_LAUNCH_CHECK();
+            hipLaunchKernelGGL((fft64k_pass_b<cb, true>), g, b, 0, st, a);
             SDRGPU_LAUNCH_CHECK();
         }
         if (two) {  // s continues only after aux's batches

@@ -411,6 +411,36 @@ void launch_any(const PllDevParams& p, const void* in, long ld_in, long n, float
 
 }  // namespace
 
+// The device forms of the libm functions the PLL chain calls (Pll::apply's arg() and
+// from_polar, src/filter/pll.rs:72-76): fn 0 = sdr_atan2f_bfx(a, b) (y = a, x = b), fn 1 =
+// sdr_sincosf_bf2(a).  Test-only (sdrgpu_debug_libm): the same inlined code as the kernels
+// above, so special operands (zeros, subnormals, infinities, NaN), the wave ballot that skips
+// their selects and the f64 / reciprocal divisions can be compared with glibc on the device.
+__global__ __launch_bounds__(256) void libm_debug_kernel(int fn, const float* __restrict__ a,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ o0,
+                                                         float* __restrict__ o1, long n) {
+    const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (fn == 0) {
+        o0[i] = sdr_atan2f_bfx(a[i], b[i]);
+    } else {
+        float sn, cs;
+        sdr_sincosf_bf2(a[i], &sn, &cs);
+        o0[i] = sn;
+        o1[i] = cs;
+    }
+}
+
+int libm_debug_launch(int fn, const float* a, const float* b, float* o0, float* o1, long n,
+                      hipStream_t s) {
+    if (n <= 0) return SDRGPU_OK;
+    hipLaunchKernelGGL(libm_debug_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fn,
+                       a, b, o0, o1, n);
+    SDRGPU_LAUNCH_CHECK();
+    return SDRGPU_OK;
+}
+
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
     if (n <= 0) return SDRGPU_OK;

@@ -28,4 +28,8 @@ struct PllChannelState {
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s);
 
+// test-only: the device atan2f (fn 0) / sincosf (fn 1) restatements over n operands
+int libm_debug_launch(int fn, const float* a, const float* b, float* o0, float* o1, long n,
+                      hipStream_t s);
+
 }  // namespace sdrgpu

@@ -36,6 +36,9 @@ FFT_OUT_DB = 1
 PLL_OUT_FILTER = 0
 PLL_OUT_STEREO_DIFF = 1
 
+DEBUG_ATAN2F = 0
+DEBUG_SINCOSF = 1
+
 BQ_IDENTITY = 0
 BQ_LOWPASS = 1
 BQ_HIGHPASS = 2
@@ -161,6 +164,7 @@ SIGNATURES = [
     ("sdrgpu_pll_reset", c_int, [_H]),
     ("sdrgpu_pll_clone", c_int, [_H, _PH]),
     ("sdrgpu_pll_destroy", None, [_H]),
+    ("sdrgpu_debug_libm", c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     # batched biquad
     ("sdrgpu_biquad_create", c_int, [c_int, c_int, POINTER(BiquadDesignC), c_float, c_size_t, _PH]),
     ("sdrgpu_biquad_coefs", c_int, [_H, POINTER(c_float)]),
