@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_fir_c2.json"))
+    ap.add_argument("--no-channel-sharded", action="store_true",
+                    help="skip the configs[4] channel-sharded FIR bank leg")
     return ap.parse_args()
 
 
@@ -88,10 +90,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv, script=None, timeout=None):
+def launch_ranks(n, argv, script=None, timeout=1800.0):
     """Run `script argv` as n rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
-    set, rendezvous on 127.0.0.1), relay their output, return the worst exit status.  The
-    parent never touches the GPU: every rank is a fresh process."""
+    set, rendezvous on 127.0.0.1), relay rank 0's output, return the first failing rank's
+    exit status.  The parent never touches the GPU: every rank is a fresh process.  The
+    children are polled together: when one exits non-zero the others are killed (a dead rank
+    would otherwise leave the rest blocked in the rendezvous), and after `timeout` seconds
+    all are killed and 124 is returned."""
+    import threading
     script = script or os.path.abspath(__file__)
     port = _free_port()
     procs = []
@@ -100,12 +106,32 @@ def launch_ranks(n, argv, script=None, timeout=None):
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate(timeout=timeout)[0]
-    rcs = [procs[0].returncode] + [p.wait(timeout=timeout) for p in procs[1:]]
-    sys.stdout.write(out.decode())
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    deadline = None if timeout is None else time.monotonic() + timeout
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [c for c in codes if c not in (None, 0)]
+        if failed:
+            rc = failed[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        if deadline is not None and time.monotonic() > deadline:
+            rc = 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+    for p in procs:
+        p.wait()
+    reader.join(timeout=10)
+    sys.stdout.write(b"".join(c for c in chunks if c).decode())
     sys.stdout.flush()
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    return rc
 
 
 def cpu_baseline(taps, seconds):
@@ -128,6 +154,197 @@ def cpu_baseline(taps, seconds):
             "kind": "port", "host": host_info(),
             "sample": f"{done} c64 samples ({done // chunk} blocks of 2^18) through the oracle "
                       f"Fir(255 taps)+Decimate(4), {el:.1f} s on 1 host core"}
+
+
+KERNEL_SOURCES = ("unnamed-rust-sdr_amd/csrc/fir_mxh.hip", "unnamed-rust-sdr_amd/csrc/fir_kernels.hpp")
+
+
+def kernel_source_sha16(root=ROOT):
+    """sha256[:16] over the headline kernel's source files: ties a committed PMC traffic
+    figure to the kernel build it was measured on (tools/pmc_to_json.py records it)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(path, log2n, algo):
+    """(traffic bytes per launch or None, traffic_source) from the committed PMC file; the
+    figure is used only when it was measured on this exact kernel source and workload."""
+    src = {"file": os.path.relpath(path, ROOT), "kernel_source_sha16": kernel_source_sha16()}
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        src["status"] = "missing"
+        return None, src
+    src.update({"measured_sha16": pm.get("kernel_source_sha16"), "method": pm.get("method"),
+                "commit": pm.get("commit")})
+    if pm.get("log2n") != log2n or pm.get("algo", "auto") != algo:
+        src["status"] = "other workload"
+        return None, src
+    if pm.get("kernel_source_sha16") != src["kernel_source_sha16"]:
+        src["status"] = "stale: measured on another kernel source"
+        return None, src
+    src["status"] = "matches this kernel source"
+    return pm.get("hbm_bytes_per_launch"), src
+
+
+def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192, log2n=16):
+    """configs[4] / north_star's multi-GPU claim, measured in the line the driver runs: an
+    8192-channel x 2^16 c64 255-tap FIR bank (D = 1) with its channels sharded over the
+    ranks (sdrgpu.shard.channel_range, one process per GPU).  Reported separately:
+      resident   every rank filters its own resident channel block (weak scaling of the
+                 bank: the per-step time is the max over ranks, the rate counts all channels);
+      rccl       the fan-out of the channel blocks from rank 0 (scatterv) and the gather of
+                 the outputs back (gatherv) over xGMI, each timed on its own (HIP events on the
+                 bank's stream, max over ranks);
+      end_to_end all channels / (scatter + one resident step + gather);
+      spot_check on rank 0 after the gather, one channel of EVERY rank's block against a
+                 float64 NumPy FIR of its input (src/filter/fir.rs:23-32 per channel).
+    Ranks sharing a GPU (a rehearsal on a smaller box) skip RCCL, which needs one device per
+    rank."""
+    import scipy.signal as ss
+    import sdrgpu
+    from sdrgpu.device import DeviceBuffer, Event, synchronize
+    from sdrgpu.shard import Comm, channel_range, unique_id
+    n = 1 << log2n
+    K = 255
+    taps = ss.firwin(K, 0.2).astype(np.float32)
+    lo, hi = channel_range(nch_total, world, rank)
+    nch = hi - lo
+    shared = world > sdrgpu.device_count()
+    bank = sdrgpu.filter.FirBank(taps, nch, sample_kind=sdrgpu.C64, device=local)
+    s = bank.stream()
+    x = DeviceBuffer.empty(nch * n, np.complex64, device=local)
+    y = DeviceBuffer.empty(nch * n, np.complex64, device=local)
+    sizes = [(b - a) * n * 8 for a, b in (channel_range(nch_total, world, r) for r in range(world))]
+    pat = synth_iq_pattern(1 << 22, seed=4000)
+    use_rccl = world > 1 and not shared
+    full_in = full_out = comm = None
+    if rank == 0 and (use_rccl or world == 1):
+        tgt = DeviceBuffer.empty(nch_total * n, np.complex64, device=local) if use_rccl else x
+        for off in range(0, nch_total * n, pat.size):
+            tgt.upload(pat[:min(pat.size, nch_total * n - off)], offset_bytes=8 * off)
+        full_in = tgt
+        full_out = DeviceBuffer.empty(nch_total * n, np.complex64, device=local) if use_rccl else y
+    elif not use_rccl:  # shared-GPU rehearsal: each rank fills its own block
+        for off in range(0, nch * n, pat.size):
+            x.upload(pat[:min(pat.size, nch * n - off)], offset_bytes=8 * off)
+    res = {"workload": f"configs[4]: {nch_total}-channel x 2^{log2n} c64 255-tap FIR bank (D=1), "
+                       "channels sharded over the ranks, one GPU per rank",
+           "channels_per_rank": [b - a for a, b in (channel_range(nch_total, world, r)
+                                                    for r in range(world))]}
+    if use_rccl:
+        ids = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        comm = Comm(local, world, rank, ids[0])
+
+        def coll(fn):  # one collective on the bank's stream, timed by events, max over ranks
+            import torch
+            e0, e1 = Event(local), Event(local)
+            comm.barrier(s)
+            e0.record(s)
+            fn()
+            e1.record(s)
+            bank.sync()
+            t = torch.tensor([e0.elapsed_ms(e1)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        scat = lambda: comm.scatterv(full_in.ptr if full_in else None, x.ptr, sizes, 0, s)
+        gath = lambda: comm.gatherv(y.ptr, full_out.ptr if full_out else None, sizes, 0, s)
+        coll(scat)  # warm-up (RCCL connection setup)
+        scatter_ms = float(np.mean([coll(scat) for _ in range(3)]))
+    synchronize(local)
+
+    def step():
+        bank.process_dev(x.ptr, n, n, y.ptr, n)
+
+    def sync():
+        bank.sync()
+        synchronize(local)
+
+    el = timed_region(step, steps, warmup, sync, dist if world > 1 else None)
+    ms = el / steps * 1e3
+    res["resident"] = {"value": round(nch_total * n / (ms * 1e-3) / 1e6, 1) if not shared else None,
+                       "unit": "complex Msamples/s (all ranks)", "ms_per_step": round(ms, 4),
+                       "roofline_frac_per_gpu": round(16 * nch * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if shared:
+        res["rccl"] = "skipped: ranks share a GPU (RCCL needs one device per rank)"
+        res["note"] = "shared-GPU rehearsal: not a throughput result"
+    if use_rccl:
+        coll(gath)
+        gather_ms = float(np.mean([coll(gath) for _ in range(3)]))
+        res["rccl"] = {"scatterv_ms": round(scatter_ms, 3), "gatherv_ms": round(gather_ms, 3),
+                       "scatterv_GBps_root": round(sum(sizes[1:]) / (scatter_ms * 1e-3) / 1e9, 1),
+                       "gatherv_GBps_root": round(sum(sizes[1:]) / (gather_ms * 1e-3) / 1e9, 1)}
+        res["end_to_end"] = {"value": round(nch_total * n / ((scatter_ms + ms + gather_ms) * 1e-3) / 1e6, 1),
+                             "unit": "complex Msamples/s", "ms": round(scatter_ms + ms + gather_ms, 3)}
+        comm.close()
+    if rank == 0 and full_out is not None:
+        # steady state: every step filtered the same resident block, so a channel's history
+        # entering the last step is the block's own last K-1 samples
+        checks = {}
+        m = 4096
+        for r in range(world):
+            a, b = channel_range(nch_total, world, r)
+            c = (a + b) // 2
+            xin = full_in.download(n, offset_bytes=8 * c * n).astype(np.complex128)
+            ref = np.convolve(np.concatenate([xin[n - (K - 1):], xin[:m]]),
+                              taps.astype(np.float64))[K - 1:K - 1 + m]
+            got = full_out.download(m, offset_bytes=8 * c * n)
+            err = float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2)))
+            checks[str(c)] = err
+            assert err <= 1e-5, (c, err)
+        res["spot_check_max_over_rms"] = checks
+    return res
+
+
+def headline_record(value, world, steps, warmup, elapsed, n, D, kern_ms, traffic, traffic_src,
+                    algo):
+    """The driver's JSON line (bench contract) for configs[1]; pure host logic (tested on
+    CPU by tests/test_bench_cpu.py)."""
+    achieved = BYTES_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e9
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "complex Msamples/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: 3 tones + 0.1 N(0,1) complex64, 2^22-sample pattern per rank tiled to the shard",
+        "config": {
+            "workload": "configs[1]: 255-tap FIR (real f32 taps, firwin 0.2) decimate-by-4 "
+                        "on complex IQ, single channel per GPU",
+            "samples_per_gpu_per_step": n,
+            "ntaps": 255, "decim": D, "sample": "c64", "taps": "f32",
+            "algorithm": algo,
+            "arith": "f32 samples and taps; on the default (MFMA) path each product is an "
+                     "fp16x2 split of the samples (per-tile power-of-two scale) times an "
+                     "fp16x2 split of the taps on v_mfma_f32_16x16x32_f16, f32 accumulate "
+                     "(DESIGN.md 3.1; within north_star's 1e-5)",
+            "parallelism": f"{world} time shards, no data-path collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel_ms": round(kern_ms, 4),
+            "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * n),
+            "fp32_tflops_direct_equiv": round(FLOPS_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e12, 2),
+        },
+    }
+    return res
 
 
 def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
@@ -231,48 +448,14 @@ def main():
     total_samples = n * args.steps * world
     value = total_samples / elapsed / 1e6
     if rank == 0:
-        achieved = BYTES_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_json):
-            try:
-                pm = json.load(open(args.pmc_json))
-                if pm.get("log2n") == args.log2n and pm.get("algo", "auto") == args.algo:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        res = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "complex Msamples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: 3 tones + 0.1 N(0,1) complex64, 2^22-sample pattern per rank tiled to the shard",
-            "config": {
-                "workload": "configs[1]: 255-tap FIR (real f32 taps, firwin 0.2) decimate-by-4 "
-                            "on complex IQ, single channel per GPU",
-                "samples_per_gpu_per_step": n,
-                "ntaps": 255, "decim": D, "sample": "c64", "taps": "f32",
-                "algorithm": args.algo,
-                "parallelism": f"{world} time shards, no data-path collective",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel_ms": round(kern_ms, 4),
-                "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * n),
-                "fp32_tflops_direct_equiv": round(FLOPS_PER_SAMPLE * n / (kern_ms * 1e-3) / 1e12, 2),
-            },
-        }
+        traffic, traffic_src = pmc_traffic(args.pmc_json, args.log2n, args.algo)
+        res = headline_record(value, world, args.steps, args.warmup, elapsed, n, D, kern_ms,
+                              traffic, traffic_src, args.algo)
+    if not args.no_channel_sharded:
+        cs = channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist)
+    if rank == 0:
+        if not args.no_channel_sharded:
+            res["channel_sharded"] = cs
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(taps, args.cpu_seconds)
         print(json.dumps(res), flush=True)

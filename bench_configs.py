@@ -385,77 +385,28 @@ def bench_c4(args):
 
 # ------------------------------------------------------------------------------ c5
 def bench_c5(args):
+    """configs[4] through bench.channel_sharded_leg (the same leg bench.py adds to the
+    driver's line): resident bank rate, RCCL scatterv / gatherv each timed on its own, end to
+    end, and a float64 spot check of one channel per rank after the gather on the root."""
     import scipy.signal as ss
-    import sdrgpu
-    from sdrgpu.device import DeviceBuffer, synchronize
-    from sdrgpu.shard import Comm, channel_range, unique_id
+    import bench
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # ranks beyond the visible GPUs share them round-robin (a rehearsal on a 1-GPU box)
+    import sdrgpu
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, sdrgpu.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    nch_total, n = args.c5_nch, 1 << args.c5_log2n
-    lo, hi = channel_range(nch_total, world, rank)
-    nch = hi - lo
-    taps = ss.firwin(255, 0.2).astype(np.float32)
-    bank = sdrgpu.filter.FirBank(taps, nch, sample_kind=sdrgpu.C64, device=local)
-    x = DeviceBuffer.empty(nch * n, device=local)
-    fill(x, nch * n, 50 + rank)
-    y = DeviceBuffer.empty(nch * n, device=local)
-
-    def step():
-        bank.process_dev(x.ptr, n, n, y.ptr, n)
-
-    wall, ms = time_events(step, bank.stream(), args.steps, args.warmup,
-                           lambda: (bank.sync(), synchronize(local)))
-    t = [ms]
-    if dist is not None:
-        import torch
-        tt = torch.tensor([ms], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = [float(tt.item())]
-    res = {"config": f"c5: 255-tap FIR bank, {nch_total} ch x 2^{args.c5_log2n} c64, {world} GPU(s), "
-                     f"{nch} resident channels per rank",
-           "metric": "complex Msamples/s (input, all ranks)",
-           "value": round(nch_total * n / (t[0] * 1e-3) / 1e6, 1) if world > 1 else round(nch * n / (ms * 1e-3) / 1e6, 1),
-           "roofline_rank0": roof(16, nch * n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
-    # spot-check one resident channel against the oracle (the rate is of checked outputs)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    ck = nch // 2
-    res["spot_check_max_over_rms"] = spot_check(pyoracle, taps, x, y, ck, n)
-    assert res["spot_check_max_over_rms"] <= 1e-5, res["spot_check_max_over_rms"]
-    if dist is not None and world > sdrgpu.device_count():
-        res["rccl"] = "skipped: ranks share a GPU (RCCL needs one device per rank)"
-        res["note"] = ("ranks share a GPU: a functional rehearsal of the sharded path; each rank's "
-                       "event window need not cover the other ranks' kernels, so value is not a "
-                       "throughput result")
-    elif dist is not None:
-        # RCCL fan-out of channel blocks from rank 0 and gather back (timed separately);
-        # uneven channel blocks (nch % world != 0) go through grouped send / recv
-        ids = [unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(ids, src=0)
-        comm = Comm(local, world, rank, ids[0])
-        sizes = [(b - a) * n * 8 for a, b in (channel_range(nch_total, world, r) for r in range(world))]
-        full = DeviceBuffer(sum(sizes), local) if rank == 0 else None
-        s = bank.stream()
-        from sdrgpu.device import Event
-        e0, e1, e2 = Event(local), Event(local), Event(local)
-        comm.barrier(s)
-        e0.record(s)
-        comm.scatterv(full.ptr if full else None, x.ptr, sizes, 0, s)
-        e1.record(s)
-        comm.gatherv(y.ptr, full.ptr if full else None, sizes, 0, s)
-        e2.record(s)
-        bank.sync()
-        res["rccl_scatter_ms"] = round(e0.elapsed_ms(e1), 3)
-        res["rccl_gather_ms"] = round(e1.elapsed_ms(e2), 3)
-        res["end_to_end_value"] = round(nch_total * n / ((t[0] + e0.elapsed_ms(e2)) * 1e-3) / 1e6, 1)
-        comm.close()
+    res = bench.channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist,
+                                    nch_total=args.c5_nch, log2n=args.c5_log2n)
+    res["config"] = res.pop("workload")
+    res["metric"] = "complex Msamples/s (input, all ranks)"
+    res["value"] = res["resident"]["value"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        taps = ss.firwin(255, 0.2).astype(np.float32)
         cores = min(os.cpu_count() or 1, 16)
         cn, cl = 4 * cores, 1 << 14
         xs = cplx_pattern(cn * cl, 9).reshape(cn, cl)
@@ -464,9 +415,8 @@ def bench_c5(args):
             pyoracle.fir_batch(taps, xs, 1, nthreads=cores)
             done += cn * cl
         el = time.perf_counter() - t0
-        from bench import host_info
         res["cpu_baseline"] = {"value": round(done / el / 1e6, 2), "unit": "complex Msamples/s",
-                               "cores": cores, "kind": "port", "host": host_info(),
+                               "cores": cores, "kind": "port", "host": bench.host_info(),
                                "sample": f"{done} samples ({cn} ch x 2^14 blocks) through the "
                                          f"oracle Fir (255 taps, one Fir per channel), {el:.1f} s"}
     if dist is not None:
@@ -523,6 +473,8 @@ def bench_src(args):
             # interpolation is per frame, shared by the channels in the wide kernel)
             fl = 2 * taps * nout * ch / (ms * 1e-3) / 1e12
             line["taps_per_output"] = round(taps, 1)
+            line["parity"] = ("unpinned vs libsamplerate: this library's own sinc tables "
+                              "(DESIGN.md 3.7); bit-exact to the oracle restatement only")
             line["roofline"] = {"bound": "fp64 issue", "achieved": round(fl, 3),
                                 "peak": 78.6, "unit": "TFLOP/s (f64 vector, AMD spec)",
                                 "frac": round(fl / 78.6, 4)}

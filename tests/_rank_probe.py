@@ -10,6 +10,8 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
+if os.environ.get("PROBE_DIE_EARLY_RANK") == os.environ["RANK"]:
+    sys.exit(5)          # dies before the rendezvous: the other ranks would block in it
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 el = bench.timed_region(lambda: None, steps=2, warmup=1, sync=lambda: None, dist=dist)

@@ -1,0 +1,60 @@
+"""CPU tests of bench.py's JSON line (the driver contract) and its evidence fields: the
+fp16x2 arithmetic label, the PMC traffic figure tied to the kernel source it was measured
+on, and the channel-sharded leg's record shape (the leg itself runs on the GPU:
+tests/test_bench_gpu.py)."""
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def test_headline_record_contract_and_labels():
+    n = 1 << 28
+    r = bench.headline_record(5.1e5, 1, 20, 3, 20 * 0.53e-3, n, 4, 0.525, 2.75e9,
+                              {"status": "matches this kernel source"}, "auto")
+    assert all(k in r for k in CONTRACT)
+    assert r["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert r["config"]["workload"].startswith("configs[1]")
+    assert "fp16x2" in r["config"]["arith"] and "f32 accumulate" in r["config"]["arith"]
+    rf = r["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["unit"] == "GB/s"
+    assert abs(rf["achieved"] - 10 * n / 0.525e-3 / 1e9) < 0.1
+    assert abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-4
+    assert rf["traffic"] == 2.75e9 and rf["traffic_source"]["status"].startswith("matches")
+    json.dumps(r)
+
+
+def test_pmc_traffic_tied_to_kernel_source(tmp_path):
+    sha = bench.kernel_source_sha16()
+    good = {"log2n": 28, "algo": "auto", "hbm_bytes_per_launch": 2.7e9,
+            "kernel_source_sha16": sha, "commit": "abc1234", "method": "m"}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(good))
+    t, src = bench.pmc_traffic(str(p), 28, "auto")
+    assert t == 2.7e9 and src["status"] == "matches this kernel source"
+    assert src["commit"] == "abc1234" and src["kernel_source_sha16"] == sha
+    p.write_text(json.dumps(dict(good, kernel_source_sha16="0" * 16)))
+    t, src = bench.pmc_traffic(str(p), 28, "auto")
+    assert t is None and src["status"].startswith("stale")
+    p.write_text(json.dumps(dict(good, log2n=20)))
+    assert bench.pmc_traffic(str(p), 28, "auto")[0] is None
+    t, src = bench.pmc_traffic(str(tmp_path / "none.json"), 28, "auto")
+    assert t is None and src["status"] == "missing"
+
+
+def test_committed_pmc_file_matches_the_shipped_kernel():
+    """profiles/pmc_fir_c2.json is the figure bench.py reports as roofline.traffic: it must
+    have been measured on the fir_mxh source in this tree (re-measure after a kernel change:
+    tools/gpu/r02_final.sh's FETCH / WRITE passes -> tools/pmc_to_json.py)."""
+    t, src = bench.pmc_traffic(os.path.join(ROOT, "profiles", "pmc_fir_c2.json"), 28, "auto")
+    assert t is not None, src
+    assert 1.0 <= t / (10 * (1 << 28)) <= 1.1

@@ -85,6 +85,35 @@ def test_launch_ranks_propagates_failure(capsys):
     assert rc == 3
 
 
+def test_launch_ranks_kills_blocked_ranks_when_one_dies_early(capsys):
+    """A rank that exits before the rendezvous leaves the others waiting in it: the launcher
+    kills them and returns the dead rank's status instead of hanging (advisor finding)."""
+    sys.path.insert(0, ROOT)
+    import time
+    import bench
+    probe = os.path.join(ROOT, "tests", "_rank_probe.py")
+    os.environ["PROBE_DIE_EARLY_RANK"] = "1"
+    try:
+        t0 = time.monotonic()
+        rc = bench.launch_ranks(3, [], script=probe, timeout=120)
+        el = time.monotonic() - t0
+    finally:
+        del os.environ["PROBE_DIE_EARLY_RANK"]
+    assert rc == 5 and el < 60
+
+
+def test_launch_ranks_timeout_kills_all(capsys):
+    sys.path.insert(0, ROOT)
+    import bench
+    probe = os.path.join(ROOT, "tests", "_rank_probe.py")
+    os.environ["PROBE_DIE_EARLY_RANK"] = "1"   # ranks 0 and 2 then wait for rank 1 forever
+    try:
+        rc = bench.launch_ranks(3, [], script=probe, timeout=0.5)
+    finally:
+        del os.environ["PROBE_DIE_EARLY_RANK"]
+    assert rc in (5, 124)
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")

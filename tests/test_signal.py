@@ -73,11 +73,29 @@ def test_cu8_take_skip_decimate_count_samples(sdr, oracle):
     from sdrgpu import _lib
     iq = _iq(1000)
     s = sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8)
+    x = oracle.u8_to_c64(iq)
     got = s.skip(1.5).take(2.0).collect()          # samples 150 .. 350 -> bytes 300 .. 700
-    assert np.array_equal(got, iq[300:700])
+    assert got.dtype == np.complex64 and np.array_equal(got, x[150:350])
     d = sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8).decimate(25.0).collect()
-    pairs = iq.reshape(-1, 2)[3::4].reshape(-1)      # kept samples wait-1, 2wait-1, ...
-    assert np.array_equal(d, pairs)
+    assert np.array_equal(d, x[3::4])                # kept samples wait-1, 2wait-1, ...
+    # iter and map hand Complex<f32> samples to user code, as RtlTcpSignal::next does
+    it = list(sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8).iter())
+    assert np.array_equal(np.array(it, np.complex64), x)
+    m = sdr.signal.from_array(100.0, iq, block=37, sample_kind=_lib.CU8).map(lambda b: b * 2)
+    assert np.array_equal(m.collect(), x * np.float32(2))
+
+
+def test_as_usize_rounds_the_f32_value():
+    """FreqSweep::new's `(t * rate).round() as usize` (sources.rs:133-134) on f32 values at
+    and above 2^23 and just below one half (advisor finding: f32 rounding of |v| + 0.5)."""
+    from sdrgpu.signal import _as_usize
+    f32 = np.float32
+    assert _as_usize(f32(2 ** 23 + 1)) == 2 ** 23 + 1
+    assert _as_usize(f32(2 ** 24 + 2)) == 2 ** 24 + 2
+    assert _as_usize(f32(0.49999997)) == 0
+    assert _as_usize(f32(0.5)) == 1 and _as_usize(f32(1.5)) == 2 and _as_usize(f32(2.5)) == 3
+    assert _as_usize(f32(-3.7)) == 0 and _as_usize(f32(0.0)) == 0
+    assert _as_usize(f32(8388609.0) * f32(1.0)) == 8388609
 
 
 def test_cu8_window_raw_frames_convert_samples(sdr, oracle):
@@ -135,3 +153,24 @@ def test_cu8_window_decimate_map_fft(sdr, oracle):
     ref = oracle.stft(oracle.u8_to_c64(iq), n, hop)
     assert y.shape == ref.shape
     assert_parity(y, ref)
+
+
+@pytest.mark.gpu
+def test_cu8_resample_with_matches_c64_path(sdr, oracle):
+    """resample_with on rtl_tcp bytes converts them as RtlTcpSignal::next does and labels the
+    output Complex<f32>: equal to the same stage fed the converted samples (advisor finding)."""
+    from sdrgpu import _lib
+    from sdrgpu.resample import ConverterType
+    iq = _iq(20000, 4)
+    x = oracle.u8_to_c64(iq)
+    rate = 1.8e6
+    a = sdr.signal.from_array(rate, iq, block=3000, sample_kind=_lib.CU8).resample_with(
+        ConverterType.Linear, 144e3)
+    b = sdr.signal.from_array(rate, x, block=3000).resample_with(ConverterType.Linear, 144e3)
+    assert a.sample_kind == _lib.C64
+    ya, yb = a.collect(), b.collect()
+    assert ya.dtype == np.complex64 and np.array_equal(ya, yb)
+    # a following decimate counts Complex samples, not byte pairs
+    d = sdr.signal.from_array(rate, iq, block=3000, sample_kind=_lib.CU8).resample_with(
+        ConverterType.Linear, 144e3).decimate(72e3).collect()
+    assert np.array_equal(d, yb[1::2])

@@ -397,6 +397,20 @@ struct sdrgpu_src_state {
         return 0;
     }
 
+    // the buffer fills recorded by sinc_append, in order: input copies and zero runs
+    int flush_appends(const float* d_in) {
+        float* w = static_cast<float*>(win[wcur].ptr);
+        for (const Append& a : appends) {
+            hipError_t e = a.src < 0
+                ? hipMemsetAsync(w + a.wpos, 0, (size_t)a.len * sizeof(float), stream.cur)
+                : hipMemcpyAsync(w + a.wpos, d_in + a.src, (size_t)a.len * sizeof(float),
+                                 hipMemcpyDeviceToDevice, stream.cur);
+            if (e != hipSuccess) return SDRGPU_SRC_ERR_BAD_STATE;
+        }
+        appends.clear();
+        return 0;
+    }
+
     // src_sinc.c's multichannel vari process loop; per output frame a descriptor of
     // calc_output_multi's taps (the samples are summed on the GPU, resample.hip)
     int sinc_process(sdrgpu_src_data& d, const float* d_in, bool in_null, float* d_out) {
@@ -427,10 +441,17 @@ struct sdrgpu_src_state {
         SincDesc* desc = static_cast<SincDesc*>(hb.ptr);
         const int max_fi = coeff_half_len << kShiftBits;
         long k = 0;
+        // an error inside the loop leaves the buffer bookkeeping where prepare_data moved it
+        // (as libsamplerate, which has already copied the data by then): enqueue the appends
+        // recorded so far so the device window matches that bookkeeping before returning
+        auto fail = [&](int st) {
+            (void)flush_appends(d_in);
+            return st;
+        };
         while (out_gen < out_count) {
             int in_hand = (b_end - b_current + b_len) % b_len;
             if (in_hand <= half) {
-                if (int st = sinc_prepare(in_count, &in_used, in_null, eoi, half)) return st;
+                if (int st = sinc_prepare(in_count, &in_used, in_null, eoi, half)) return fail(st);
                 in_hand = (b_end - b_current + b_len) % b_len;
                 if (in_hand <= half) break;
             }
@@ -440,7 +461,7 @@ struct sdrgpu_src_state {
             const double float_increment = index_inc * (src_ratio < 1.0 ? src_ratio : 1.0);
             const int inc = (int)std::lrint(float_increment * kFpOne);
             const int start = (int)std::lrint(input_index * float_increment * kFpOne);
-            if ((size_t)k >= cap_frames) return SDRGPU_SRC_ERR_BAD_INTERNAL_STATE;
+            if ((size_t)k >= cap_frames) return fail(SDRGPU_SRC_ERR_BAD_INTERNAL_STATE);
             SincDesc& o = desc[k++];
             // left half (with the underflow skip of calc_output_multi)
             int fi = start;
@@ -474,14 +495,8 @@ struct sdrgpu_src_state {
         last_position = input_index;
         last_ratio = src_ratio;
         // enqueue: the buffer fills (input copies / zeros), the descriptors, the sums
+        if (int st = flush_appends(d_in)) return st;
         float* w = static_cast<float*>(win[wcur].ptr);
-        for (const Append& a : appends) {
-            hipError_t e = a.src < 0
-                ? hipMemsetAsync(w + a.wpos, 0, (size_t)a.len * sizeof(float), stream.cur)
-                : hipMemcpyAsync(w + a.wpos, d_in + a.src, (size_t)a.len * sizeof(float),
-                                 hipMemcpyDeviceToDevice, stream.cur);
-            if (e != hipSuccess) return SDRGPU_SRC_ERR_BAD_STATE;
-        }
         if (k > 0) {
             if (d_desc.ensure((size_t)k * sizeof(SincDesc))) return SDRGPU_SRC_ERR_MALLOC_FAILED;
             if (hipMemcpyAsync(d_desc.ptr, desc, (size_t)k * sizeof(SincDesc),

@@ -24,6 +24,7 @@ Sources: from_array (FromIter, sources.rs:6-36), freq (sources.rs:196-221), freq
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, Iterator, Optional
 
 import numpy as np
@@ -73,11 +74,12 @@ class Signal:
         return self._blocks()
 
     def iter(self):
+        """Signal::iter: samples one by one (rtl_tcp bytes as Complex<f32>, rtltcp.rs:156-164)."""
         for b in self.blocks():
-            yield from b
+            yield from (_cu8_values(b) if self.sample_kind == _lib.CU8 else b)
 
     def collect(self) -> np.ndarray:
-        bl = [b for b in self.blocks()]
+        bl = [(_cu8_values(b) if self.sample_kind == _lib.CU8 else b) for b in self.blocks()]
         return np.concatenate(bl) if bl else np.zeros(0)
 
     # ---- combinators ----
@@ -172,7 +174,9 @@ class Signal:
                     if b is None:
                         exhausted = True
                         break
-                    b = np.asarray(b)
+                    # rtl_tcp bytes reach SampleRate as the Complex<f32> samples
+                    # RtlTcpSignal::next yields (rtltcp.rs:156-164), two channels
+                    b = _cu8_values(b) if up.sample_kind == _lib.CU8 else np.asarray(b)
                     if sr is None:
                         cplx = np.iscomplexobj(b)
                         ch = 2 if cplx else (1 if b.ndim == 1 else b.shape[1])
@@ -193,7 +197,15 @@ class Signal:
                         yield out.reshape(-1)
                     else:
                         yield out
-        return Signal(float(np.float32(rate)), gen, self.sample_kind)
+        # the output is converted samples: Complex<f32> for complex (or rtl_tcp) input, f32 for
+        # mono, frames of `channels` f32 otherwise -- never raw CU8 byte pairs
+        if self.sample_kind in (_lib.C64, _lib.CU8):
+            out_kind = _lib.C64
+        elif self.sample_kind == _lib.F32:
+            out_kind = _lib.F32
+        else:
+            out_kind = None
+        return Signal(float(np.float32(rate)), gen, out_kind)
 
     def window(self, duration: float) -> "Signal":
         cap = int(round(duration * self._rate))
@@ -202,11 +214,12 @@ class Signal:
         return s
 
     def map(self, fn: Callable) -> "Signal":
+        """Signal::map: fn sees Complex<f32> samples for rtl_tcp input (rtltcp.rs:156-164)."""
         up = self
 
         def gen():
             for b in up.blocks():
-                yield fn(b)
+                yield fn(_cu8_values(b) if up.sample_kind == _lib.CU8 else b)
         return Signal(self._rate, gen, None)
 
     def take(self, duration: float) -> "Signal":
@@ -336,6 +349,15 @@ def freq(rate: float, f: float, phase: float, n: int, block: int = DEFAULT_BLOCK
     return from_array(rate, _polar_unit(phs), block)
 
 
+def _as_usize(v) -> int:
+    """`v.round() as usize` for an f32 v (FreqSweep::new, sources.rs:133-134): round half away
+    from zero, then the saturating cast (negative -> 0).  |v| + 0.5 is formed in f64 -- in
+    f32 it would itself round (2^23 + 1 -> 2^23 + 2, 0.49999997 -> 1)."""
+    v = float(np.float32(v))
+    r = math.floor(abs(v) + 0.5)
+    return int(r) if v > 0 else 0
+
+
 def freq_sweep(rate: float, df: float, warmup: bool, start: float, end: float,
                block: int = DEFAULT_BLOCK) -> Signal:
     """signal::freq_sweep(rate, df, warmup, start..end) (sources.rs:181-194) through
@@ -350,9 +372,7 @@ def freq_sweep(rate: float, df: float, warmup: bool, start: float, end: float,
     warmupt = f32(1.0) / f32(df) if warmup else f32(0.0)
     fend_t = f32(warmupt + endt)
 
-    def as_usize(v):  # `(v * rate).round() as usize`: half away from zero, saturating
-        r = np.floor(np.abs(v) + 0.5) * np.sign(v)
-        return int(r) if r > 0 else 0
+    as_usize = _as_usize
     rate32 = f32(rate)
     fstart = as_usize(f32(warmupt * rate32))
     fend = as_usize(f32(fend_t * rate32))
