@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--c5-log2n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds: skip the c3 spot check")
     ap.add_argument("--gpus", type=int, default=1,
                     help="c5 only: run as this many ranks (self-launched, one process per GPU)")
     return ap.parse_args()
@@ -168,7 +169,7 @@ def bench_c3(args):
         ref = pyoracle.fft_frame(span).astype(np.complex128)
         got = y.download(N, offset_bytes=8 * N * j)
         worst = max(worst, float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2))))
-    assert worst <= 1e-5, worst
+    assert worst <= 1e-5 or args.no_check, worst
     res = {"config": "c3: 64k-point STFT, 50% overlap, fftshift + 1/sqrt(N), 2^28 c64 samples",
            "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
            "frames": nf, "roofline": roof(24, n, ms), "wall_ms_per_step": round(wall * 1e3, 3),

@@ -282,6 +282,56 @@ def test_stft_c3_multibatch_schedule(sdr, oracle, mode):
         assert_parity(y2[0], ref, what="c3 next-call frame")
 
 
+@pytest.mark.parametrize("nframes", [1, 2, 3, 9, 17, 64])
+def test_stft_64k_small_blocks(sdr, oracle, nframes):
+    """64K STFT blocks of 1-64 frames (one partial scratch batch, fewer workgroups than
+    CUs, the stream-start history frame included): every frame against the oracle."""
+    from sdrgpu.device import DeviceBuffer
+    n, hop = 65536, 32768
+    total = hop * nframes
+    rng = np.random.default_rng(nframes)
+    x = cplx(rng, total)
+    s = sdr.fft.Stft(n, hop)
+    nf = s.output_len(total)
+    assert nf == nframes
+    dx = DeviceBuffer.from_numpy(x)
+    dy = DeviceBuffer.empty(nf * n)
+    assert s.process_dev(dx.ptr, total, dy.ptr, nf) == nf
+    s.sync()
+    for j in range(nf):
+        y = dy.download(n, offset_bytes=8 * n * j)
+        assert_parity(y, oracle.fft_frame(_c3_frame_span(x, j, n, hop)), what=f"frame {j}")
+
+
+def test_stft_64k_repeat_bit_identical(sdr):
+    """The same 300-frame block through fresh 64K STFT handles 6 times back to back (warm
+    caches, scratch slab reused across the two-stream batches): every output word of every
+    run must equal the first run's (the four-step is deterministic whatever workgroup runs a
+    piece), and the first run's frames match NumPy."""
+    from sdrgpu.device import DeviceBuffer
+    n, hop, nfr = 65536, 32768, 300
+    total = hop * nfr
+    rng = np.random.default_rng(11)
+    x = cplx(rng, total)
+    dx = DeviceBuffer.from_numpy(x)
+    dy = DeviceBuffer.empty(nfr * n)
+    first = None
+    for rep in range(6):
+        s = sdr.fft.Stft(n, hop)
+        assert s.process_dev(dx.ptr, total, dy.ptr, nfr) == nfr
+        s.sync()
+        y = dy.download(nfr * n)
+        if first is None:
+            first = y
+            for j in (0, 1, 150, nfr - 1):
+                span = _c3_frame_span(x, j, n, hop).astype(np.complex128)
+                ref = np.fft.fftshift(np.fft.fft(span)) / np.sqrt(n)
+                assert_parity(y[j * n:(j + 1) * n], ref, what=f"frame {j}")
+        else:
+            assert np.array_equal(y.view(np.uint64), first.view(np.uint64)), f"run {rep} differs"
+        s.close()
+
+
 def _check_db(y_db, ref_c, what):
     """dB output vs the oracle's complex bins: the magnitudes 10^(dB/20) within the FIR/FFT
     parity bound (1e-5 of RMS), and 20 log10 |X| (src/plot/complexseries.rs:90-92)
