@@ -44,8 +44,12 @@ FLOPS_PER_SAMPLE = 255 * 4 / 4 # direct form, kept outputs only
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 200 timed steps (~0.1 s at configs[1]): the per-launch kernel time settles over the first
+    # ~100 launches (0.513 ms mean over 20 steps, 0.500 over 100, 0.495 over 300 on one box,
+    # profiles/r03_bench_steps.txt), and the fixed start/stop cost of the timed region is
+    # amortised; 20 warmup steps
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=28, help="input samples per GPU per step")
     ap.add_argument("--algo", default="auto", choices=["auto", "direct", "os", "mx"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -191,7 +195,7 @@ def pmc_traffic(path, log2n, algo):
     return pm.get("hbm_bytes_per_launch"), src
 
 
-def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192, log2n=16):
+def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192, log2n=16, check=True):
     """configs[4] / north_star's multi-GPU claim, measured in the line the driver runs: an
     8192-channel x 2^16 c64 255-tap FIR bank (D = 1) with its channels sharded over the
     ranks (sdrgpu.shard.channel_range, one process per GPU).  Reported separately:
@@ -296,7 +300,7 @@ def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192,
             got = full_out.download(m, offset_bytes=8 * c * n)
             err = float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2)))
             checks[str(c)] = err
-            assert err <= 1e-5, (c, err)
+            assert err <= 1e-5 or not check, (c, err)
         res["spot_check_max_over_rms"] = checks
     return res
 

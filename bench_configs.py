@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--c5-log2n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds: skip the c3 spot check")
+    ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds: skip the c3 / c5 spot checks")
     ap.add_argument("--gpus", type=int, default=1,
                     help="c5 only: run as this many ranks (self-launched, one process per GPU)")
     return ap.parse_args()
@@ -400,7 +400,7 @@ def bench_c5(args):
         import torch.distributed as dist
         dist.init_process_group("gloo")
     res = bench.channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist,
-                                    nch_total=args.c5_nch, log2n=args.c5_log2n)
+                                    nch_total=args.c5_nch, log2n=args.c5_log2n, check=not args.no_check)
     res["config"] = res.pop("workload")
     res["metric"] = "complex Msamples/s (input, all ranks)"
     res["value"] = res["resident"]["value"]

@@ -130,6 +130,18 @@ i1 = s.index("            }\n            if (!ld_run) {", i0)
 s = s[:i0] + s[i1:]
 open(p, 'w').write(s)
 PY
+  elif [ $v = mfma4 ]; then  # the two taps-hi x samples-lo MFMAs dropped (4 of 6 per chunk; wrong precision: MFMA-count probe)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """                    if (!U8) {
+                        cr[j] = mfma(ah[c], f[1], cr[j]);
+                        ci[j] = mfma(ah[c], f[3], ci[j]);
+                    }"""
+assert old in s
+s = s.replace(old, "")
+open(p, 'w').write(s)
+PY
   elif [ $v = wgtime ]; then  # per-workgroup start/end s_memrealtime (100 MHz) into out[0..511]: tail census
     python3 - $src <<'PY'
 import sys

@@ -16,7 +16,7 @@ timeout -k 10 300 python bench.py > $O/bench.jsonl 2> $O/bench.err || { tail -20
 cut -c1-900 $O/bench.jsonl
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline --steps 20 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 4; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 4; }
 cd $R
 timeout -k 10 300 python -u bench.py --gpus 2 --no-cpu-baseline --steps 10 --warmup 2 > $O/bench_2rank.jsonl 2> $O/bench_2rank.err || { tail -20 $O/bench_2rank.err; exit 9; }
 cut -c1-1500 $O/bench_2rank.jsonl
