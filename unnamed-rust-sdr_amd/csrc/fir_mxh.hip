@@ -490,11 +490,23 @@ void fir_mxh_kernel(MxhParams p) {
                     yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
                 }
                 if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
-                    f32x4* o4 = reinterpret_cast<f32x4*>(out + m);
+                    // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
+                    // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
+                    // line) and the second those of the odd-v blocks (steady-state probe: 0.472
+                    // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
+                    const bool ev = (v & 1) == 0;
                     const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
                     const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                    __builtin_nontemporal_store(y0, o4);
-                    __builtin_nontemporal_store(y1, o4 + 1);
+                    f32x4 rx;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
+                            __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
+                    const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
+                    f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
+                    f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
+                    __builtin_nontemporal_store(ev ? y0 : rx, o4);
+                    __builtin_nontemporal_store(ev ? rx : y1, p4);
                 } else {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
