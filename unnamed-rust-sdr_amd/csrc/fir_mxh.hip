@@ -435,13 +435,20 @@ void fir_mxh_kernel(MxhParams p) {
                         f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
             };
             read_frags(fb[0], 0, 0);
+            // D = 1: column set j + 1's chunk 0 reads the window span of set j's last chunk
+            // (256 samples = NCH - 1 chunks of 32 further), so that fragment is not re-read:
+            // the slot of chunk i is (i - j) & 1
+            constexpr bool kShare = D == 1 && 32 * (NCH - 1) == 256;
 #pragma unroll
             for (int i = 0; i < CS * NCH; ++i) {
                 const int j = i / NCH, c = i % NCH;
                 {
-                    if (i + 1 < CS * NCH) read_frags(fb[(i + 1) & 1], (i + 1) % NCH, (i + 1) / NCH);
+                    const int ni = i + 1;
+                    const bool reuse = kShare && ni % NCH == 0;
+                    if (ni < CS * NCH && !reuse)
+                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], ni % NCH, ni / NCH);
                     __builtin_amdgcn_sched_barrier(0);
-                    const u32x4(&f)[4] = fb[i & 1];
+                    const u32x4(&f)[4] = fb[(kShare ? i - j : i) & 1];
                     cr[j] = mfma(al[c], f[0], cr[j]);
                     ci[j] = mfma(al[c], f[2], ci[j]);
                     if (!U8) {
