@@ -148,7 +148,7 @@ import sys
 p = sys.argv[1]; s = open(p).read()
 old = "    const int lane = threadIdx.x & 63;"
 assert old in s
-s = s.replace(old, "    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();\n" + old, 1)
+s = s.replace(old, "    const unsigned long long t_wg0 = __builtin_amdgcn_s_memrealtime();\n" + old, 1)
 old2 = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
 assert old2 in s
 s = s.replace(old2, """    __syncthreads();
@@ -157,7 +157,7 @@ s = s.replace(old2, """    __syncthreads();
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         unsigned long long* o = reinterpret_cast<unsigned long long*>(p.out) + 2 * blockIdx.x;
-        o[0] = t_start | ((unsigned long long)(xcc & 7) << 56);
+        o[0] = t_wg0 | ((unsigned long long)(xcc & 7) << 56);
         o[1] = t_end;
     }
 """ + old2, 1)

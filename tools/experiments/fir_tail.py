@@ -24,7 +24,9 @@ for off in range(0, n, 1 << 22):
     x.upload(pat, offset_bytes=8 * off)
 y = DeviceBuffer.empty(n // 4, np.complex64, device=0)
 e0, e1 = Event(0), Event(0)
-for rep in range(6):
+REPS = int(os.environ.get('TAIL_REPS', '6'))
+summ = []
+for rep in range(REPS):
     e0.record(fir.stream())
     fir.process_dev(x.ptr, n, y.ptr, n // 4)
     e1.record(fir.stream())
@@ -40,6 +42,12 @@ for rep in range(6):
     byx = collections.defaultdict(list)
     for xi, ei in zip(xcc, (e - s0) / 100.0):
         byx[xi].append(ei)
-    print(f"rep {rep}: event {ev_us:.1f} us, span {ends[-1]:.1f} us, start spread {(s.max() - s0) / 100.0:.1f} us, end "
+    summ.append((ev_us, ends[-1], float(np.mean(ends)), ends[0]))
+    if rep >= REPS - 4 or rep < 2:
+      print(f"rep {rep}: event {ev_us:.1f} us, span {ends[-1]:.1f} us, start spread {(s.max() - s0) / 100.0:.1f} us, end "
           f"min/p10/p50/p90/max {ends[0]:.1f}/{ends[25]:.1f}/{ends[128]:.1f}/{ends[230]:.1f}/{ends[-1]:.1f} us; "
           "per-XCD mean end " + " ".join(f"{k}:{np.mean(v):.1f}" for k, v in sorted(byx.items())))
+a = np.array(summ[len(summ) // 2:])
+print(f"last {len(a)} reps: event {a[:, 0].mean():.1f} us, last end {a[:, 1].mean():.1f}, mean end {a[:, 2].mean():.1f}, "
+      f"first end {a[:, 3].mean():.1f} us -> a balanced split would save {(a[:, 1] - a[:, 2]).mean():.1f} us "
+      f"({100 * (a[:, 1] - a[:, 2]).mean() / a[:, 0].mean():.1f} %)")
