@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_fir_c2.json"))
+    ap.add_argument("--leg-timeout", type=float, default=240.0,
+                    help="seconds before a hung channel-sharded (RCCL) leg is abandoned")
     ap.add_argument("--no-channel-sharded", action="store_true",
                     help="skip the configs[4] channel-sharded FIR bank leg")
     return ap.parse_args()
@@ -305,6 +307,37 @@ def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192,
     return res
 
 
+def run_guarded(fn, seconds, rank, on_timeout):
+    """Run the channel-sharded leg so that it cannot take the headline line down with it.  Its
+    multi-rank RCCL part only runs on a node with one GPU per rank, so a failure there must not
+    cost the configs[1] result: an exception becomes {"error": ...} in the line, and a hang (a
+    peer that died inside a collective) fires a per-rank watchdog after `seconds` that calls
+    on_timeout() (rank 0 prints the line without the leg) and ends the process with status 0,
+    so every rank of the launch exits instead of waiting on the others."""
+    import threading
+
+    def fire():
+        sys.stderr.write(f"bench.py rank {rank}: channel-sharded leg still running after {seconds:.0f} s; "
+                         "abandoning it\n")
+        try:
+            on_timeout()
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+    timer = threading.Timer(seconds, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal to it
+        sys.stderr.write(f"bench.py rank {rank}: channel-sharded leg failed: {e!r}\n")
+        return {"error": repr(e)[:300]}
+    finally:
+        timer.cancel()
+
+
 def headline_record(value, world, steps, warmup, elapsed, n, D, kern_ms, traffic, traffic_src,
                     algo):
     """The driver's JSON line (bench contract) for configs[1]; pure host logic (tested on
@@ -456,7 +489,12 @@ def main():
         res = headline_record(value, world, args.steps, args.warmup, elapsed, n, D, kern_ms,
                               traffic, traffic_src, args.algo)
     if not args.no_channel_sharded:
-        cs = channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist)
+        def abandon():
+            if rank == 0:
+                res["channel_sharded"] = {"error": f"abandoned after {args.leg_timeout:.0f} s (RCCL leg hung)"}
+                print(json.dumps(res), flush=True)
+        cs = run_guarded(lambda: channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist),
+                         args.leg_timeout, rank, abandon)
     if rank == 0:
         if not args.no_channel_sharded:
             res["channel_sharded"] = cs

@@ -58,3 +58,21 @@ def test_committed_pmc_file_matches_the_shipped_kernel():
     t, src = bench.pmc_traffic(os.path.join(ROOT, "profiles", "pmc_fir_c2.json"), 28, "auto")
     assert t is not None, src
     assert 1.0 <= t / (10 * (1 << 28)) <= 1.1
+
+
+def test_channel_sharded_leg_guard_exception_and_hang():
+    """bench.run_guarded: a failing leg becomes an "error" entry; a hung leg (a peer that died
+    inside an RCCL collective) fires the watchdog, which emits the line and exits with 0."""
+    import subprocess
+    import sys
+    import bench
+    out = bench.run_guarded(lambda: 1 / 0, 30.0, 0, lambda: None)
+    assert "ZeroDivisionError" in out["error"]
+    assert bench.run_guarded(lambda: {"ok": 1}, 30.0, 0, lambda: None) == {"ok": 1}
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench.run_guarded(lambda: time.sleep(60), 0.5, 0, lambda: print('LINE', flush=True)); "
+            "print('NOT REACHED')") % bench.ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30)
+    assert p.returncode == 0, p.stderr
+    assert "LINE" in p.stdout and "NOT REACHED" not in p.stdout
+    assert "abandoning" in p.stderr
