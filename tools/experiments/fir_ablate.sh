@@ -174,6 +174,57 @@ for old, new in (("constexpr int kWaves = 8;               // two waves per SIMD
     s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
+  elif [ $v = mfmaord ] || [ $v = dualacc ]; then  # MFMA operand order (switching energy)
+    python3 - $src $v <<'PY'
+import sys
+p, v = sys.argv[1], sys.argv[2]; s = open(p).read()
+old = """                    cr[j] = mfma(al[c], f[0], cr[j]);
+                    ci[j] = mfma(al[c], f[2], ci[j]);
+                    if (!U8) {
+                        cr[j] = mfma(ah[c], f[1], cr[j]);
+                        ci[j] = mfma(ah[c], f[3], ci[j]);
+                    }
+                    cr[j] = mfma(ah[c], f[0], cr[j]);
+                    ci[j] = mfma(ah[c], f[2], ci[j]);"""
+assert old in s
+if v == 'mfmaord':  # A changes once per chunk (al, al, ah, ah, ah, ah)
+    new = """                    cr[j] = mfma(al[c], f[0], cr[j]);
+                    ci[j] = mfma(al[c], f[2], ci[j]);
+                    cr[j] = mfma(ah[c], f[0], cr[j]);
+                    ci[j] = mfma(ah[c], f[2], ci[j]);
+                    if (!U8) {
+                        cr[j] = mfma(ah[c], f[1], cr[j]);
+                        ci[j] = mfma(ah[c], f[3], ci[j]);
+                    }"""
+else:  # second accumulator pair: consecutive MFMAs share their B operand
+    new = """                    cr[j] = mfma(al[c], f[0], cr[j]);
+                    cr2[j] = mfma(ah[c], f[0], cr2[j]);
+                    ci[j] = mfma(al[c], f[2], ci[j]);
+                    ci2[j] = mfma(ah[c], f[2], ci2[j]);
+                    if (!U8) {
+                        cr[j] = mfma(ah[c], f[1], cr[j]);
+                        ci[j] = mfma(ah[c], f[3], ci[j]);
+                    }"""
+    o2 = """            f32x4 cr[CS], ci[CS];
+#pragma unroll
+            for (int j = 0; j < CS; ++j) {
+                cr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }"""
+    assert o2 in s
+    s = s.replace(o2, o2.replace("f32x4 cr[CS], ci[CS];", "f32x4 cr[CS], ci[CS], cr2[CS], ci2[CS];").replace(
+        "ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};", "ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};\n                cr2[j] = ci2[j] = cr[j];"))
+    o3 = "            const int so = -(s_cur + p.sh);"
+    assert o3 in s
+    s = s.replace(o3, """#pragma unroll
+            for (int j = 0; j < CS; ++j) {
+                cr[j] += cr2[j];
+                ci[j] += ci2[j];
+            }
+""" + o3)
+s = s.replace(old, new)
+open(p, 'w').write(s)
+PY
   fi
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
