@@ -174,6 +174,19 @@ for old, new in (("constexpr int kWaves = 8;               // two waves per SIMD
     s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
+  elif [ $v = lomask2 ] || [ $v = lomask3 ]; then  # low mantissa bits of the lo planes cleared (MFMA switching energy)
+    python3 - $src $v <<'PY'
+import sys
+p, v = sys.argv[1], sys.argv[2]; s = open(p).read()
+m = {'lomask2': '0xFFFCFFFCu', 'lomask3': '0xFFF8FFF8u'}[v]
+old = "    lo = pk_rtz(a - lo_f(hi), b - hi_f(hi));"
+assert old in s
+s = s.replace(old, "    lo = pk_rtz(a - lo_f(hi), b - hi_f(hi)) & " + m + ";")
+old2 = "                al[c][jj] = lw;"
+assert old2 in s
+s = s.replace(old2, "                al[c][jj] = lw & " + m + ";")
+open(p, 'w').write(s)
+PY
   elif [ $v = mfmaord ] || [ $v = dualacc ]; then  # MFMA operand order (switching energy)
     python3 - $src $v <<'PY'
 import sys
