@@ -332,6 +332,48 @@ def test_stft_64k_repeat_bit_identical(sdr):
         s.close()
 
 
+def test_stft_64k_dynamic_range_and_nan(sdr, oracle):
+    """configs[2]'s 64K four-step at whole-stream scales from 1e-30 to 1e30, with an all-zero
+    frame and a strong tone over a 1e-6 noise floor (120 dB of range in every frame): within
+    the FFT parity bound against the float64 DFT; a NaN sample turns exactly the frames that
+    contain it into NaN (rustfft's butterflies spread it over every bin, fft.rs:10-12) and
+    leaves the others finite."""
+    from sdrgpu.device import DeviceBuffer
+    n, hop, nfr = 65536, 32768, 12
+    total = hop * nfr
+    rng = np.random.default_rng(64)
+    t = np.arange(total)
+    base = (np.exp(2j * np.pi * 0.1234567 * t) + 1e-6 * cplx(rng, total)).astype(np.complex64)
+    base[4 * hop:6 * hop] = 0          # frames 4 and 5 partly, frame 5 wholly (span 4..5) zero
+    for scale in (1e-30, 1.0, 1e30):
+        x = (base * np.float32(scale)).astype(np.complex64)
+        s = sdr.fft.Stft(n, hop)
+        dx = DeviceBuffer.from_numpy(x)
+        dy = DeviceBuffer.empty(nfr * n)
+        assert s.process_dev(dx.ptr, total, dy.ptr, nfr) == nfr
+        s.sync()
+        y = dy.download(nfr * n).reshape(nfr, n)
+        assert np.isfinite(y).all(), scale
+        assert not y[5].any(), "all-zero frame"
+        for j in (0, 3, 4, 6, nfr - 1):
+            span = _c3_frame_span(x, j, n, hop).astype(np.complex128)
+            ref = np.fft.fftshift(np.fft.fft(span)) / np.sqrt(n)
+            assert_parity(y[j], ref, what=f"scale {scale} frame {j}")
+    x = base.copy()
+    x[7 * hop + 123] = np.nan          # inside frames 7 and 8 (spans [6h, 8h) and [7h, 9h))
+    s = sdr.fft.Stft(n, hop)
+    dx = DeviceBuffer.from_numpy(x)
+    dy = DeviceBuffer.empty(nfr * n)
+    assert s.process_dev(dx.ptr, total, dy.ptr, nfr) == nfr
+    s.sync()
+    y = dy.download(nfr * n).reshape(nfr, n)
+    for j in range(nfr):
+        if j in (7, 8):
+            assert np.isnan(y[j]).all(), f"frame {j} holds the NaN"
+        else:
+            assert np.isfinite(y[j]).all(), f"frame {j} does not"
+
+
 def _check_db(y_db, ref_c, what):
     """dB output vs the oracle's complex bins: the magnitudes 10^(dB/20) within the FIR/FFT
     parity bound (1e-5 of RMS), and 20 log10 |X| (src/plot/complexseries.rs:90-92)
