@@ -1,5 +1,5 @@
 #!/bin/bash
-# configs[2] evidence for the BFP24 scratch: rocprof kernel stats of bench_configs c3 (20 steps)
+# configs[2] evidence: rocprof kernel stats of bench_configs c3 (20 steps)
 # and FETCH_SIZE / WRITE_SIZE passes (2 steps), summaries under gpurun_out/$OUT/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
