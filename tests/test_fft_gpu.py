@@ -334,10 +334,14 @@ def test_stft_64k_repeat_bit_identical(sdr):
 
 def test_stft_64k_dynamic_range_and_nan(sdr, oracle):
     """configs[2]'s 64K four-step at whole-stream scales from 1e-30 to 1e30, with an all-zero
-    frame and a strong tone over a 1e-6 noise floor (120 dB of range in every frame): within
-    the FFT parity bound against the float64 DFT; a NaN sample turns exactly the frames that
-    contain it into NaN (rustfft's butterflies spread it over every bin, fft.rs:10-12) and
-    leaves the others finite."""
+    frame and a strong tone over a 1e-6 noise floor (120 dB of range in every frame), against
+    the float64 DFT.  A tone's spectrum is one peak ~sqrt(N) = 256 times the bins' RMS, so any
+    f32 FFT (rustfft's included) rounds that bin at ~1e-7 of the PEAK, i.e. 2-4e-5 of the RMS
+    (profiles/r03s3_stft64k_tone_precision.txt: the same at every scale, with or without the
+    noise floor): the max error is judged against the peak here, the L2 error against the norm
+    (SURVEY 8c's two measures, the first one normalised where it is well posed).  A NaN
+    sample turns exactly the frames that contain it into NaN (the butterflies spread it over
+    every bin) and leaves the others finite."""
     from sdrgpu.device import DeviceBuffer
     n, hop, nfr = 65536, 32768, 12
     total = hop * nfr
@@ -358,7 +362,10 @@ def test_stft_64k_dynamic_range_and_nan(sdr, oracle):
         for j in (0, 3, 4, 6, nfr - 1):
             span = _c3_frame_span(x, j, n, hop).astype(np.complex128)
             ref = np.fft.fftshift(np.fft.fft(span)) / np.sqrt(n)
-            assert_parity(y[j], ref, what=f"scale {scale} frame {j}")
+            d = np.abs(y[j].astype(np.complex128) - ref)
+            peak = np.abs(ref).max()
+            assert d.max() <= 1e-5 * peak, (scale, j, d.max() / peak)
+            assert np.linalg.norm(d) <= 1e-5 * np.linalg.norm(ref), (scale, j)
     x = base.copy()
     x[7 * hop + 123] = np.nan          # inside frames 7 and 8 (spans [6h, 8h) and [7h, 9h))
     s = sdr.fft.Stft(n, hop)
