@@ -141,3 +141,75 @@ def test_random_pll_partitions_bit_exact(sdr, oracle, i):
     ref, rl = oracle.pll_batch(oracle_params(oracle), x, nthreads=8)
     assert np.array_equal(lk, rl), f"lock flags, case {i} cuts={cuts}"
     assert np.array_equal(y, ref), f"outputs, case {i} cuts={cuts}"
+
+
+N_STFT = 12
+N_BIQUAD = 12
+N_SRC = 16
+
+
+@pytest.mark.parametrize("i", range(N_STFT))
+def test_random_stft_stream(sdr, oracle, i):
+    """Window(n) + Decimate(hop) + fft (src/signal/adapters/mod.rs:270-303, 13-41) at random
+    (n, hop) over ragged blocks: every frame against the oracle's STFT."""
+    rng = np.random.default_rng(5000 + i)
+    n = int(rng.choice([int(rng.integers(2, 300)), 256, 1000, 1024, int(rng.integers(300, 3000)), 4096]))
+    hop = int(rng.integers(1, 2 * n + 1))
+    total = int(rng.integers(0, 6 * n + 3 * hop))
+    x = ((rng.standard_normal(total) + 1j * rng.standard_normal(total))).astype(np.complex64)
+    s = sdr.fft.Stft(n, hop)
+    cuts = _blocks(rng, total)
+    parts = [s.process(x[a0:a1]) for a0, a1 in zip(cuts[:-1], cuts[1:])]
+    parts = [p for p in parts if p.size]
+    ref = oracle.stft(x, n, hop, nthreads=8)
+    if not parts:
+        assert ref.shape[0] == 0, (n, hop, total)
+        return
+    y = np.concatenate(parts, axis=0)
+    assert y.shape == ref.shape, (y.shape, ref.shape, n, hop, total, cuts)
+    for j in range(ref.shape[0]):
+        assert_parity(y[j], ref[j], what=f"stft case {i}: n={n} hop={hop} frame {j} cuts={cuts}")
+
+
+@pytest.mark.parametrize("i", range(N_BIQUAD))
+def test_random_biquad_stream_bit_exact(sdr, oracle, i):
+    """BiquadD::design + Biquad::apply (src/filter/biquad.rs:25-56,83-155) at random designs,
+    sample kinds, channel counts and block partitions: array_equal to the oracle."""
+    rng = np.random.default_rng(6000 + i)
+    rate = float(rng.choice([48000.0, 144000.0, 1.8e6]))
+    kind = str(rng.choice(["LowPass", "HighPass", "BandPass", "Notch", "Lr"]))
+    f = sdr.filter
+    if kind == "Lr":
+        d = f.BiquadD.Lr(float(rng.uniform(10e-6, 200e-6)))
+    else:
+        d = getattr(f.BiquadD, kind)(float(rng.uniform(0.001, 0.45)) * rate, float(rng.uniform(0.3, 8.0)))
+    sk = int(rng.integers(0, 2))
+    nch = int(rng.choice([1, 3, 64, 65, 200]))
+    n = int(rng.choice([1, 17, 1000, 4001]))
+    bq = d.design(rate, sample_kind=sk, nch=nch)
+    if sk:
+        x = (rng.standard_normal((nch, n)) + 1j * rng.standard_normal((nch, n))).astype(np.complex64)
+    else:
+        x = rng.standard_normal((nch, n)).astype(np.float32)
+    cuts = _blocks(rng, n)
+    y = np.concatenate([bq.process(x[:, a0:a1]) for a0, a1 in zip(cuts[:-1], cuts[1:]) if a1 > a0], axis=1)
+    c = d.to_c()
+    for ch in sorted({0, nch // 2, nch - 1}):
+        ref = oracle.biquad_run(c.kind, c.freq, c.q, rate, x[ch])
+        np.testing.assert_array_equal(y[ch], ref, err_msg=f"biquad case {i}: {kind} sk={sk} ch {ch} cuts={cuts}")
+
+
+@pytest.mark.parametrize("i", range(N_SRC))
+def test_random_resampler_bit_exact(sdr, oracle, i):
+    """SampleRate::process (src/resample.rs:32-110) at random converter, ratio, channel count,
+    input block lengths and output capacities, call by call against the oracle (libsamplerate's
+    bookkeeping restated; the sinc tables are this library's own)."""
+    from test_resample import _run_both
+    rng = np.random.default_rng(7000 + i)
+    conv = int(rng.choice([0, 1, 2, 3, 4, 2, 4]))
+    ratio = float(rng.choice([float(rng.uniform(0.02, 1.0)), float(rng.uniform(1.0, 8.0)),
+                              48000 * 3.0 / 1.8e6, 48000 / 144000.0]))
+    ch = int(rng.choice([1, 2, 3, 5]))
+    n = int(rng.integers(1, 4000))
+    x = rng.standard_normal((n, ch)).astype(np.float32)
+    _run_both(sdr, oracle, conv, ch, ratio, x, rng)
