@@ -174,6 +174,21 @@ for old, new in (("constexpr int kWaves = 8;               // two waves per SIMD
     s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
+  elif [ $v = mfma16 ]; then  # each 16x16x32 MFMA as two 16x16x16 ones over the two K halves of the same fragments
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);"""
+assert old in s
+s = s.replace(old, """    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    const f16x8 a8 = __builtin_bit_cast(f16x8, a), b8 = __builtin_bit_cast(f16x8, b);
+    const f16x4 alo = {a8[0], a8[1], a8[2], a8[3]}, ahi = {a8[4], a8[5], a8[6], a8[7]};
+    const f16x4 blo = {b8[0], b8[1], b8[2], b8[3]}, bhi = {b8[4], b8[5], b8[6], b8[7]};
+    c = __builtin_amdgcn_mfma_f32_16x16x16f16(alo, blo, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(ahi, bhi, c, 0, 0, 0);""")
+open(p, 'w').write(s)
+PY
   elif [ $v = lomask2 ] || [ $v = lomask3 ]; then  # low mantissa bits of the lo planes cleared (MFMA switching energy)
     python3 - $src $v <<'PY'
 import sys
