@@ -174,3 +174,19 @@ def test_cu8_resample_with_matches_c64_path(sdr, oracle):
     d = sdr.signal.from_array(rate, iq, block=3000, sample_kind=_lib.CU8).resample_with(
         ConverterType.Linear, 144e3).decimate(72e3).collect()
     assert np.array_equal(d, yb[1::2])
+
+
+def test_fm_receiver_designs_host_only(sdr):
+    """sdrgpu.fm mirrors src/main.rs:41-60's designs and refuses input that is not rtl_tcp
+    bytes (host logic only; the chain itself runs in tests/test_fm_chain_gpu.py)."""
+    from sdrgpu import _lib, fm
+    from sdrgpu.signal import from_array
+    d = fm.discriminator_design()
+    assert (d.reference, d.gain) == (0.0, 0.035)
+    p = fm.pilot_design()
+    assert (p.reference, p.gain) == (19000.0, 0.0002)
+    # BiquadD::Lr(1.0 / (75.0 * 0.001 * 0.001)) evaluated in f32, as the reference's literals are
+    dr = np.float32(1.0) / (np.float32(75.0) * np.float32(0.001) * np.float32(0.001))
+    assert np.float32(fm.deemphasis().freq) == dr and fm.deemphasis().kind == _lib.BQ_LR
+    with pytest.raises(_lib.SdrGpuError):
+        fm.receiver(from_array(1.8e6, np.zeros(16, np.complex64)))
