@@ -307,6 +307,20 @@ def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192,
     return res
 
 
+def init_gloo_quiet(dist):
+    """dist.init_process_group("gloo") with file descriptor 1 pointed at stderr meanwhile: gloo
+    prints "[Gloo] Rank r is connected to ..." on stdout, and the driver reads rank 0's stdout
+    for the ONE JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        dist.init_process_group("gloo")
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def run_guarded(fn, seconds, rank, on_timeout):
     """Run the channel-sharded leg so that it cannot take the headline line down with it.  Its
     multi-rank RCCL part only runs on a node with one GPU per rank, so a failure there must not
@@ -428,7 +442,7 @@ def main():
         # rank coordination only (barrier, max-time): the path has no data exchange, so
         # no RCCL collective is used; gloo keeps torch's own HIP runtime off the GPU.
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        init_gloo_quiet(dist)
 
     import scipy.signal as ss
     import sdrgpu

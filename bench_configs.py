@@ -398,7 +398,7 @@ def bench_c5(args):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        bench.init_gloo_quiet(dist)
     res = bench.channel_sharded_leg(args.steps, args.warmup, world, rank, local, dist,
                                     nch_total=args.c5_nch, log2n=args.c5_log2n, check=not args.no_check)
     res["config"] = res.pop("workload")

@@ -76,3 +76,25 @@ def test_channel_sharded_leg_guard_exception_and_hang():
     assert p.returncode == 0, p.stderr
     assert "LINE" in p.stdout and "NOT REACHED" not in p.stdout
     assert "abandoning" in p.stderr
+
+
+def test_gloo_init_keeps_stdout_clean(tmp_path):
+    """bench.init_gloo_quiet: a 2-rank gloo rendezvous prints nothing on stdout (the driver
+    reads rank 0's stdout for its one JSON line); gloo's connect message goes to stderr."""
+    import subprocess
+    import sys
+    import bench
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; import torch.distributed as dist; "
+            "bench.init_gloo_quiet(dist); dist.barrier(); print('OK', flush=True); "
+            "dist.destroy_process_group()") % bench.ROOT
+    port = bench._free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (out, err) in zip(procs, outs):
+        assert p.returncode == 0, err
+        assert out.strip() == "OK", out
