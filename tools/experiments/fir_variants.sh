@@ -1,0 +1,29 @@
+#!/bin/bash
+# Build copies of the headline FIR kernel with one constant changed into
+# tools/experiments/abl/lib_<v>.so (never into the product library), plus libbase.so = the
+# product build.  VARIANTS="run2 run4 run16" (kRunTiles), wg4 (two 4-wave
+# workgroups per CU).  Run one with:
+#   python tools/experiments/run_with_lib.py tools/experiments/abl/lib_<v>.so bench.py ...
+set -e
+cd "$(dirname "$0")/../.."
+mkdir -p tools/experiments/abl
+make -C unnamed-rust-sdr_amd -s
+cp unnamed-rust-sdr_amd/libsdrgpu.so tools/experiments/abl/libbase.so
+OBJS=$(ls unnamed-rust-sdr_amd/build/*.o | grep -v fir_mxh.o)
+for v in ${VARIANTS:-run2 run4 run16}; do
+  src=tools/experiments/abl/fir_mxh_$v.hip
+  cp unnamed-rust-sdr_amd/csrc/fir_mxh.hip $src
+  case $v in
+    run*) n=${v#run}; sed -i "s/^constexpr int kRunTiles = 8;/constexpr int kRunTiles = $n;/" $src
+          grep -q "kRunTiles = $n;" $src ;;
+    wg4) # two 4-wave workgroups per CU (finer end-time granularity), 2 x CUs workgroups
+          sed -i "s/^constexpr int kWaves = 8; .*/constexpr int kWaves = 4;/; s/std::min((long)cus, ceil_div(p.units, kWaves))/std::min(2L * cus, ceil_div(p.units, kWaves))/" $src
+          grep -q "kWaves = 4;" $src && grep -q "2L \* cus" $src ;;
+    *) echo "unknown variant $v"; exit 1 ;;
+  esac
+  /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result \
+    -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so \
+    tools/experiments/abl/fir_mxh_$v.o $OBJS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  echo "built lib_$v.so"
+done
