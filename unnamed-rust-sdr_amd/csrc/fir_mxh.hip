@@ -46,7 +46,12 @@ constexpr int kBlock = 64 * kWaves;
 // D = 1 tiles: three 256-output column sets share one staged window (2.48 vs 2.62 ms with one
 // set at configs[4]; profiles/r02_fir_d1_cs.txt), and 6 groups keep one raw tile in flight
 constexpr int kCs1 = 3;
-constexpr int kRunTiles = 8;
+// D = 4 runs: 2 tiles for c64 samples (a CU's eight waves then stream one 128 KiB window:
+// 0.461-0.464 vs 0.486-0.488 ms at 8 tiles, 0.486 at 3, 0.481 at 4, 0.534 at 1; steady-state
+// A/B in profiles/r03s4_run_length_ab.txt), 8 for the u8 ingest (0.227-0.229 vs 0.232-0.234
+// at 2)
+constexpr int kRunTiles = 2;
+constexpr int kRunTilesU8 = 8;
 
 // CS: 256-output MFMA column sets per tile.  D = 1 stages the window's history once for CS
 // column sets (the history is 1.5x a 256-sample set, so re-staging it per set dominated)
@@ -615,10 +620,10 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     const int cs = D == 1 ? kCs1 : 1;
     p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     const long W = (long)kWaves * cus;
-    // D = 4: runs of kRunTiles tiles dealt in per-CU blocks (0.516-0.525 vs 0.556-0.559 ms with
-    // one long range per wave at configs[1]; profiles/r02_fir_runs.txt).  D = 1 banks keep
-    // whole-channel units grid-strided (no gain from runs there).
-    const int run = D == 4 ? kRunTiles : 0;
+    // D = 4: runs of kRunTiles tiles dealt in per-CU blocks (round 2: 0.516-0.525 vs
+    // 0.556-0.559 ms with one long range per wave at configs[1], profiles/r02_fir_runs.txt).
+    // D = 1 banks keep whole-channel units grid-strided (no gain from runs there).
+    const int run = D == 4 ? (u8 ? kRunTilesU8 : kRunTiles) : 0;
     long spc = nch >= W ? 1 : ceil_div(W, nch);
     spc = std::max(1L, std::min(spc, p.tpc));
     p.seg_tiles = std::max(1L, ceil_div(p.tpc, spc));
