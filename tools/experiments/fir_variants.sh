@@ -1,7 +1,8 @@
 #!/bin/bash
 # Build copies of the headline FIR kernel with one constant changed into
 # tools/experiments/abl/lib_<v>.so (never into the product library), plus libbase.so = the
-# product build.  VARIANTS="run2 run4 run16" (kRunTiles), wg4 (two 4-wave
+# product build.  VARIANTS="run2 run4 run16" (kRunTiles), u8runN (kRunTilesU8),
+# d1runN (D = 1 banks dealt in blocked runs of N tiles), wg4 (two 4-wave
 # workgroups per CU).  Run one with:
 #   python tools/experiments/run_with_lib.py tools/experiments/abl/lib_<v>.so bench.py ...
 set -e
@@ -14,8 +15,12 @@ for v in ${VARIANTS:-run2 run4 run16}; do
   src=tools/experiments/abl/fir_mxh_$v.hip
   cp unnamed-rust-sdr_amd/csrc/fir_mxh.hip $src
   case $v in
-    run*) n=${v#run}; sed -i "s/^constexpr int kRunTiles = 8;/constexpr int kRunTiles = $n;/" $src
+    run*) n=${v#run}; sed -i "s/^constexpr int kRunTiles = [0-9]*;/constexpr int kRunTiles = $n;/" $src
           grep -q "kRunTiles = $n;" $src ;;
+    u8run*) n=${v#u8run}; sed -i "s/^constexpr int kRunTilesU8 = [0-9]*;/constexpr int kRunTilesU8 = $n;/" $src
+          grep -q "kRunTilesU8 = $n;" $src ;;
+    d1run*) n=${v#d1run}; sed -i "s/(u8 ? kRunTilesU8 : kRunTiles) : 0;/(u8 ? kRunTilesU8 : kRunTiles) : $n;/" $src
+          grep -q "kRunTiles) : $n;" $src ;;
     wg4) # two 4-wave workgroups per CU (finer end-time granularity), 2 x CUs workgroups
           sed -i "s/^constexpr int kWaves = 8; .*/constexpr int kWaves = 4;/; s/std::min((long)cus, ceil_div(p.units, kWaves))/std::min(2L * cus, ceil_div(p.units, kWaves))/" $src
           grep -q "kWaves = 4;" $src && grep -q "2L \* cus" $src ;;

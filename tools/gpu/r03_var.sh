@@ -17,8 +17,9 @@ import json
 for l in open('$O/$v.$i.jsonl'):
     l=l.strip()
     if not l.startswith('{'): continue
-    d=json.loads(l); r=d.get('roofline',{})
-    print(d.get('config',{}).get('workload','')[:12], r.get('kernel_ms'), r.get('frac'))
+    d=json.loads(l); r=d.get('roofline',{}); c=d.get('channel_sharded',{}).get('resident',{})
+    w=d.get('config',{}); w=w.get('workload','') if isinstance(w,dict) else w
+    print(w[:12], r.get('kernel_ms'), r.get('frac'), 'c5', c.get('ms_per_step'), c.get('roofline_frac_per_gpu'))
 ")" | tee -a $O/summary.txt
   done
 done
