@@ -15,6 +15,8 @@ for v in ${VARIANTS:-run2 run4 run16}; do
   src=tools/experiments/abl/fir_mxh_$v.hip
   cp unnamed-rust-sdr_amd/csrc/fir_mxh.hip $src
   case $v in
+    gsrun*) n=${v#gsrun}; sed -i "s/^constexpr int kRunTiles = [0-9]*;/constexpr int kRunTiles = $n;/; s/^constexpr int kRunTilesU8 = [0-9]*;/constexpr int kRunTilesU8 = $n;/; s/^    p.blocked = run > 0;/    p.blocked = 0;/" $src
+          grep -q "kRunTiles = $n;" $src && grep -q "p.blocked = 0;" $src ;;
     run*) n=${v#run}; sed -i "s/^constexpr int kRunTiles = [0-9]*;/constexpr int kRunTiles = $n;/" $src
           grep -q "kRunTiles = $n;" $src ;;
     u8run*) n=${v#u8run}; sed -i "s/^constexpr int kRunTilesU8 = [0-9]*;/constexpr int kRunTilesU8 = $n;/" $src
@@ -24,6 +26,25 @@ for v in ${VARIANTS:-run2 run4 run16}; do
     wg4) # two 4-wave workgroups per CU (finer end-time granularity), 2 x CUs workgroups
           sed -i "s/^constexpr int kWaves = 8; .*/constexpr int kWaves = 4;/; s/std::min((long)cus, ceil_div(p.units, kWaves))/std::min(2L * cus, ceil_div(p.units, kWaves))/" $src
           grep -q "kWaves = 4;" $src && grep -q "2L \* cus" $src ;;
+    xcd) # XCD-aware range map: the 8 XCDs (dispatch slot b % 8) each stream one contiguous eighth
+          python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+a = "    const long wave = (long)blockIdx.x * kWaves + wv;"
+assert a in s
+s = s.replace(a, a + "\n    const long bxr = gridDim.x % 8 == 0 ? (long)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : (long)blockIdx.x;")
+for o, n in (("((long)blockIdx.x + 1) * p.units / gridDim.x", "(bxr + 1) * p.units / gridDim.x"),
+             ("(long)blockIdx.x * p.units / gridDim.x + wv", "bxr * p.units / gridDim.x + wv")):
+    assert o in s
+    s = s.replace(o, n)
+open(p, 'w').write(s)
+PY
+          ;;
+    gstride) # runs dealt grid-strided (all CUs stream one chip-wide window) instead of per-WG ranges
+          sed -i "s/^    p.blocked = run > 0;/    p.blocked = 0;/" $src
+          grep -q "p.blocked = 0;" $src ;;
+    noprio) sed -i "s/^    if (wv >= kWaves \/ 2) __builtin_amdgcn_s_setprio(1);//" $src
+          ! grep -q "s_setprio(1);" $src ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result \

@@ -46,10 +46,12 @@ constexpr int kBlock = 64 * kWaves;
 // D = 1 tiles: three 256-output column sets share one staged window (2.48 vs 2.62 ms with one
 // set at configs[4]; profiles/r02_fir_d1_cs.txt), and 6 groups keep one raw tile in flight
 constexpr int kCs1 = 3;
-// D = 4 runs: 2 tiles for c64 samples (a CU's eight waves then stream one 128 KiB window:
-// 0.461-0.464 vs 0.486-0.488 ms at 8 tiles, 0.486 at 3, 0.481 at 4, 0.534 at 1; steady-state
-// A/B in profiles/r03s4_run_length_ab.txt), 8 for the u8 ingest (0.227-0.229 vs 0.232-0.234
-// at 2)
+// D = 4 runs.  c64 samples: runs of 2 tiles dealt grid-strided, so at any moment the whole
+// chip streams one contiguous window (2048 waves x 16 KiB): 0.441 ms, against 0.460 for the
+// same runs in per-workgroup ranges, 0.486-0.488 for per-workgroup runs of 8 (round 3 s3), and
+// 0.478 / 0.486-0.491 / 0.528 for grid-strided runs of 4 / 8 / 1 (steady-state A/B,
+// profiles/r03s4_run_length_ab.txt).  u8 ingest: per-workgroup runs of 8 (every variant
+// within noise there).
 constexpr int kRunTiles = 2;
 constexpr int kRunTilesU8 = 8;
 
@@ -281,7 +283,8 @@ void fir_mxh_kernel(MxhParams p) {
     // Units (runs of seg_tiles tiles of one channel) are dealt to waves either in per-
     // workgroup contiguous ranges (p.blocked: wave w of the workgroup takes units w, w+8, ...,
     // so a CU's eight waves stream eight ADJACENT runs -- one HBM locality window per CU) or
-    // grid-strided.  The wave walks its units as ONE stream of tiles: three cursors (tile k
+    // grid-strided (wave b * 8 + w takes units b * 8 + w + k * 8 * grid: one chip-wide window at
+    // a time).  The wave walks its units as ONE stream of tiles: three cursors (tile k
     // computed and stored, k+1 staged, k+2 loading) advance together, so the raw-tile
     // prefetch crosses run boundaries; a run's first window re-reads the H samples before it
     // (issued one tile ahead, into the history registers).
@@ -620,9 +623,9 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     const int cs = D == 1 ? kCs1 : 1;
     p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     const long W = (long)kWaves * cus;
-    // D = 4: runs of kRunTiles tiles dealt in per-CU blocks (round 2: 0.516-0.525 vs
-    // 0.556-0.559 ms with one long range per wave at configs[1], profiles/r02_fir_runs.txt).
-    // D = 1 banks keep whole-channel units grid-strided (no gain from runs there).
+    // D = 4: runs of kRunTiles tiles (c64: grid-strided; u8: per-CU blocks, round 2: 0.516-0.525
+    // vs 0.556-0.559 ms with one long range per wave, profiles/r02_fir_runs.txt).  D = 1 banks
+    // keep whole-channel units grid-strided (runs measured no faster there).
     const int run = D == 4 ? (u8 ? kRunTilesU8 : kRunTiles) : 0;
     long spc = nch >= W ? 1 : ceil_div(W, nch);
     spc = std::max(1L, std::min(spc, p.tpc));
@@ -630,7 +633,7 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     if (run > 0) p.seg_tiles = std::max(1L, std::min<long>(run, p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
-    p.blocked = run > 0;
+    p.blocked = run > 0 && u8;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
 #define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
     hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
