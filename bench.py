@@ -197,6 +197,19 @@ def pmc_traffic(path, log2n, algo):
     return pm.get("hbm_bytes_per_launch"), src
 
 
+def channel_block_bytes(nch_total, world, n):
+    """Per-rank byte counts of the channel blocks scatterv / gatherv move (c64 channels of n
+    samples, split by sdrgpu.shard.channel_range; zero for ranks with no channel)."""
+    from sdrgpu.shard import channel_range
+    return [(b - a) * n * 8 for a, b in (channel_range(nch_total, world, r) for r in range(world))]
+
+
+def channel_offset_bytes(c, n):
+    """Byte offset of channel c in the root's packed all-channel buffer (the layout scatterv /
+    gatherv use: rank blocks in rank order, channels contiguous inside a block)."""
+    return 8 * c * n
+
+
 def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192, log2n=16, check=True):
     """configs[4] / north_star's multi-GPU claim, measured in the line the driver runs: an
     8192-channel x 2^16 c64 255-tap FIR bank (D = 1) with its channels sharded over the
@@ -225,7 +238,7 @@ def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192,
     s = bank.stream()
     x = DeviceBuffer.empty(nch * n, np.complex64, device=local)
     y = DeviceBuffer.empty(nch * n, np.complex64, device=local)
-    sizes = [(b - a) * n * 8 for a, b in (channel_range(nch_total, world, r) for r in range(world))]
+    sizes = channel_block_bytes(nch_total, world, n)
     pat = synth_iq_pattern(1 << 22, seed=4000)
     use_rccl = world > 1 and not shared
     full_in = full_out = comm = None
@@ -296,10 +309,10 @@ def channel_sharded_leg(steps, warmup, world, rank, local, dist, nch_total=8192,
         for r in range(world):
             a, b = channel_range(nch_total, world, r)
             c = (a + b) // 2
-            xin = full_in.download(n, offset_bytes=8 * c * n).astype(np.complex128)
+            xin = full_in.download(n, offset_bytes=channel_offset_bytes(c, n)).astype(np.complex128)
             ref = np.convolve(np.concatenate([xin[n - (K - 1):], xin[:m]]),
                               taps.astype(np.float64))[K - 1:K - 1 + m]
-            got = full_out.download(m, offset_bytes=8 * c * n)
+            got = full_out.download(m, offset_bytes=channel_offset_bytes(c, n))
             err = float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2)))
             checks[str(c)] = err
             assert err <= 1e-5 or not check, (c, err)
@@ -321,13 +334,18 @@ def init_gloo_quiet(dist):
         os.close(saved)
 
 
+LEG_HUNG_EXIT = 3  # exit status of a rank whose channel-sharded leg hung (run_guarded)
+
+
 def run_guarded(fn, seconds, rank, on_timeout):
     """Run the channel-sharded leg so that it cannot take the headline line down with it.  Its
     multi-rank RCCL part only runs on a node with one GPU per rank, so a failure there must not
     cost the configs[1] result: an exception becomes {"error": ...} in the line, and a hang (a
     peer that died inside a collective) fires a per-rank watchdog after `seconds` that calls
-    on_timeout() (rank 0 prints the line without the leg) and ends the process with status 0,
-    so every rank of the launch exits instead of waiting on the others."""
+    on_timeout() (rank 0 prints the line with channel_sharded.error) and ends the process with
+    status LEG_HUNG_EXIT, so every rank of the launch exits instead of waiting on the others and
+    the hang shows up as a FAILED run (the launcher and the driver see the non-zero status) --
+    the main thread may still be stuck inside a collective or a GPU call at that point."""
     import threading
 
     def fire():
@@ -338,7 +356,7 @@ def run_guarded(fn, seconds, rank, on_timeout):
         finally:
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(LEG_HUNG_EXIT)
 
     timer = threading.Timer(seconds, fire)
     timer.daemon = True

@@ -360,12 +360,30 @@ def bench_c4(args):
     units = nch * n
     fir_check = spot_check(pyoracle, taps, x, mf, nch // 3, n)
     assert fir_check <= 1e-5, fir_check
+    # PLL spot check at the timed width: a fresh handle of the same design (same kernel, all
+    # nch channels) over the first 16 Ki samples of the resident matched-filter output; a few
+    # channels' outputs and lock flags array_equal to the oracle PLL (src/filter/pll.rs:70-85)
+    m = min(n, 1 << 14)
+    pll_v = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
+                        f.BiquadD.LowPass(20000.0, 0.7)).design(rate, nch=nch)
+    pll_v.set_stream(bank.stream())
+    pll_v.process_dev(mf.ptr, n, m, out.ptr, lk.ptr, n)
+    bank.sync()
+    p = pyoracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
+    chans = sorted({0, nch // 3, nch // 2 + 1, nch - 1})
+    mfs = np.stack([mf.download(m, offset_bytes=8 * c * n) for c in chans])
+    ref_out, ref_lk = pyoracle.pll_batch(p, mfs, nthreads=len(chans))
+    got_out = np.stack([out.download(m, dtype=np.float32, offset_bytes=4 * c * n) for c in chans])
+    got_lk = np.stack([lk.download(m, dtype=np.uint8, offset_bytes=c * n) for c in chans])
+    pll_mism = int(np.sum(got_out != ref_out) + np.sum(got_lk != ref_lk))
+    assert pll_mism == 0, f"c4 PLL spot check: {pll_mism} outputs / lock flags differ"
     res = {"config": f"c4: 255-tap matched filter + PLL FM demod (src/main.rs:41-46), {nch} ch x 2^{args.c4_log2n}",
            "metric": "complex Msamples/s (input, all channels)", "value": round(units / (ms * 1e-3) / 1e6, 1),
            "roofline": roof(12, units, ms), "fir_ms": round(ms_fir, 3), "pll_ms": round(ms - ms_fir, 3),
            "pll_ns_per_sample_chain": round((ms - ms_fir) * 1e6 / n, 2),
            "note": "PLL is bound by its loop-carried latency (ns per sample per channel chain), not HBM",
-           "wall_ms_per_step": round(wall * 1e3, 3), "fir_spot_check_max_over_rms": fir_check}
+           "wall_ms_per_step": round(wall * 1e3, 3), "fir_spot_check_max_over_rms": fir_check,
+           "pll_spot_check": f"channels {chans} x {m} samples: outputs + lock flags array_equal to the oracle"}
     if not args.no_cpu_baseline:
         cores = min(os.cpu_count() or 1, 16)
         cn, cl = cores, 1 << 14

@@ -432,6 +432,23 @@ int sdrgpu_comm_gatherv(sdrgpu_comm* c, const void* d_send, void* d_recv, const 
 int sdrgpu_comm_barrier(sdrgpu_comm* c, void* hip_stream);
 void sdrgpu_comm_destroy(sdrgpu_comm* c);
 
+/* The point-to-point plan scatterv (gather = 0) / gatherv (gather = 1) issue on `rank`:
+ * one op per non-empty transfer -- a zero-byte rank (nch < nranks) takes part in no send,
+ * receive or copy.  kind: SDRGPU_COMM_SEND / RECV (peer = the other rank) or
+ * SDRGPU_COMM_COPY (the root's own block, a device-local copy; peer = root); offset = the
+ * byte offset of the block in the ROOT's buffer (displs[r]; 0 on the non-root side, whose
+ * buffer holds only its own block).  Host-only arithmetic, no device work: *n_ops = the op
+ * count (ops may be NULL to ask for it; SDRGPU_ERR_INVALID if max_ops is short). */
+typedef struct {
+    int32_t kind;
+    int32_t peer;
+    size_t offset;
+    size_t bytes;
+} sdrgpu_comm_op;
+enum { SDRGPU_COMM_SEND = 0, SDRGPU_COMM_RECV = 1, SDRGPU_COMM_COPY = 2 };
+int sdrgpu_comm_plan_v(int nranks, int rank, int root, int gather, const size_t* bytes,
+                       const size_t* displs, sdrgpu_comm_op* ops, int max_ops, int* n_ops);
+
 #ifdef __cplusplus
 }
 #endif

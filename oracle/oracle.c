@@ -538,7 +538,9 @@ size_t oracle_freq_sweep(float rate, float df, int warmup, float start, float en
     return total;
 }
 
-/* RtlTcpSignal::next (rtltcp.rs:156-164): (v - 128) / 128 */
+/* Host glibc atan2f (fn 0) or sinf / cosf (fn 1) over n arguments: what Rust's f32::atan2 /
+ * sin / cos call on x86-64 Linux (pll.rs:71-78); the checker for the device restatements in
+ * libm_glibc.h (tests/test_libm_gpu.py). */
 void oracle_libm(int fn, const float* a, const float* b, float* out0, float* out1, size_t n) {
     for (size_t i = 0; i < n; ++i) {
         if (fn == 0) {
@@ -550,6 +552,7 @@ void oracle_libm(int fn, const float* a, const float* b, float* out0, float* out
     }
 }
 
+/* RtlTcpSignal::next (rtltcp.rs:156-164): (v - 128) / 128 */
 void oracle_u8_to_c64(const uint8_t* in, size_t n, float* out) {
     for (size_t i = 0; i < 2 * n; ++i) out[i] = ((float)in[i] - 128.0f) / 128.0f;
 }

@@ -62,7 +62,8 @@ def test_committed_pmc_file_matches_the_shipped_kernel():
 
 def test_channel_sharded_leg_guard_exception_and_hang():
     """bench.run_guarded: a failing leg becomes an "error" entry; a hung leg (a peer that died
-    inside an RCCL collective) fires the watchdog, which emits the line and exits with 0."""
+    inside an RCCL collective) fires the watchdog, which emits the line and exits NON-zero
+    (bench.LEG_HUNG_EXIT), so the hang is reported as a failed run, not a clean one."""
     import subprocess
     import sys
     import bench
@@ -73,7 +74,7 @@ def test_channel_sharded_leg_guard_exception_and_hang():
             "bench.run_guarded(lambda: time.sleep(60), 0.5, 0, lambda: print('LINE', flush=True)); "
             "print('NOT REACHED')") % bench.ROOT
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == bench.LEG_HUNG_EXIT != 0, (p.returncode, p.stderr)
     assert "LINE" in p.stdout and "NOT REACHED" not in p.stdout
     assert "abandoning" in p.stderr
 

@@ -56,6 +56,68 @@ def test_shard_ranges(sdr):
         assert all(lo % align == 0 for lo, _ in rs)
 
 
+@pytest.mark.parametrize("nch,world", [(8192, 8), (8192, 3), (1024, 3), (5, 8), (1, 4)])
+def test_channel_range_uneven_and_empty(sdr, nch, world):
+    """Balanced split: sizes differ by at most one, the first ranks take the remainder, and
+    with nch < world the last ranks get an empty block (5 channels over 8 ranks)."""
+    from sdrgpu.shard import channel_range
+    sizes = [b - a for a, b in (channel_range(nch, world, r) for r in range(world))]
+    assert sum(sizes) == nch and max(sizes) - min(sizes) <= 1
+    assert sizes == sorted(sizes, reverse=True)
+    if nch < world:
+        assert sizes.count(0) == world - nch
+
+
+@pytest.mark.parametrize("nch,world", [(8192, 8), (8192, 3), (5, 8), (1, 4), (3, 2)])
+@pytest.mark.parametrize("root", ["first", "last"])
+@pytest.mark.parametrize("gather", [False, True], ids=["scatterv", "gatherv"])
+def test_comm_plan_v_splits(sdr, nch, world, root, gather):
+    """sdrgpu_comm_plan_v -- the ops sdrgpu_comm_scatterv / gatherv issue (abi_comm.cpp) --
+    for uneven and zero-channel ranks, on every rank: each non-empty rank pairs one op with
+    the root at its displacement, an empty rank takes part in nothing, and the root's blocks
+    tile its packed buffer exactly (no gap, no overlap)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from sdrgpu.shard import COPY, RECV, SEND, channel_range, counts_displs, plan_v
+    n = 1 << 10
+    root = 0 if root == "first" else world - 1
+    sizes = bench.channel_block_bytes(nch, world, n)
+    _, displs = counts_displs(sizes)
+    plans = [plan_v(world, r, root, gather, sizes) for r in range(world)]
+    mine, theirs = (RECV, SEND) if gather else (SEND, RECV)
+    for r in range(world):
+        if r == root:
+            continue
+        if sizes[r] == 0:
+            assert plans[r] == [], (r, plans[r])   # the empty-rank path: no send / recv
+            continue
+        assert plans[r] == [(theirs, root, 0, sizes[r])]
+        assert (mine, r, displs[r], sizes[r]) in plans[root]
+    spans = sorted((off, off + nb) for k, p, off, nb in plans[root])
+    assert all(nb > 0 for *_, nb in plans[root])
+    assert len(plans[root]) == sum(1 for v in sizes if v)
+    assert [k for k, p, *_ in plans[root] if p == root] == ([COPY] if sizes[root] else [])
+    assert spans[0][0] == 0 and spans[-1][1] == sum(sizes)
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    # bench.py's post-gather spot check reads channel c at channel_offset_bytes(c, n): that
+    # must be inside rank r's block at its scatterv displacement
+    for r in range(world):
+        lo, hi = channel_range(nch, world, r)
+        for c in {lo, (lo + hi) // 2, hi - 1} if hi > lo else ():
+            off = bench.channel_offset_bytes(c, n)
+            assert off == displs[r] + 8 * n * (c - lo)
+            assert displs[r] <= off and off + 8 * n <= displs[r] + sizes[r]
+
+
+def test_comm_plan_v_rejects_bad_args(sdr):
+    from sdrgpu._lib import SdrGpuError
+    from sdrgpu.shard import plan_v
+    with pytest.raises(SdrGpuError):
+        plan_v(4, 0, 4, False, [8, 8, 8, 8])    # root out of range
+    with pytest.raises(SdrGpuError):
+        plan_v(4, 4, 0, True, [8, 8, 8, 8])     # rank out of range
+
+
 def test_launch_ranks_spawns_world(capsys):
     """`bench.py --gpus N` without torchrun starts N rank processes itself (the driver's
     N-GPU invocation shape) and relays rank 0's JSON line."""

@@ -150,16 +150,19 @@ def test_firbank_d1_channelizer_full_width(sdr, oracle):
     assert l2 <= 1e-5
 
 
-def test_c4_matched_filter_into_pll_chain(sdr, oracle):
+@pytest.mark.parametrize("nch,n,cut", [(128, 16384, 6000), (1024, 9000, 3002)],
+                         ids=["nch128", "nch1024_configs3"])
+def test_c4_matched_filter_into_pll_chain(sdr, oracle, nch, n, cut):
     """configs[3]: matched-filter bank (D = 1, MFMA) -> batched PLL (src/main.rs:41-49) on
-    device buffers.  The bank is checked against the oracle's Fir within 1e-5; the PLL is
-    bit-exact to the oracle PLL fed the same (downloaded) bank output."""
+    device buffers, at 128 channels and at configs[3]'s stated width of 1024 channels
+    (16 PLL workgroups, n >= 8192 in two ragged even blocks).  The bank is checked against
+    the oracle's Fir within 1e-5; the PLL outputs and lock flags are bit-exact to the oracle
+    PLL (src/filter/pll.rs:70-85) fed the same (downloaded) bank output."""
     from sdrgpu import _lib
     from sdrgpu.device import DeviceBuffer
     import scipy.signal as ss
     from test_pll_gpu import RATE, fm_channels, main_rs_design, oracle_params
-    rng = np.random.default_rng(45)
-    nch, n = 128, 16384
+    rng = np.random.default_rng(45 + nch)
     x = fm_channels(rng, nch, n)
     taps = ss.firwin(255, 0.2).astype(np.float32)
     b = bank(sdr, taps, nch)
@@ -168,7 +171,7 @@ def test_c4_matched_filter_into_pll_chain(sdr, oracle):
     dy = DeviceBuffer.empty(nch * n, np.complex64)
     do = DeviceBuffer.empty(nch * n, np.float32)
     dl = DeviceBuffer.empty(nch * n, np.uint8)
-    for a, e in ((0, 6000), (6000, n)):
+    for a, e in ((0, cut), (cut, n)):
         assert b.process_dev(dx.ptr + 8 * a, n, e - a, dy.ptr + 8 * a, n) == e - a
         assert b.last_algorithm() == _lib.FIR_MATRIX
         b.sync()

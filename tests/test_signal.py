@@ -98,6 +98,23 @@ def test_as_usize_rounds_the_f32_value():
     assert _as_usize(f32(8388609.0) * f32(1.0)) == 8388609
 
 
+def test_as_usize_saturates_like_rust_as():
+    """Rust's `f32 as usize` saturates: NaN -> 0, -inf -> 0, +inf -> usize::MAX (advisor
+    finding r3); freq_sweep with df = 0 and rate = 0 (inf * 0 = NaN) is an empty sweep."""
+    import warnings
+    from sdrgpu import _lib
+    from sdrgpu.signal import USIZE_MAX, _as_usize, freq_sweep
+    f32 = np.float32
+    assert _as_usize(f32(np.nan)) == 0 and _as_usize(f32(-np.inf)) == 0
+    assert _as_usize(f32(np.inf)) == USIZE_MAX == 2 ** 64 - 1
+    assert _as_usize(f32(3.0e38)) == USIZE_MAX and _as_usize(f32(2.0 ** 40)) == 2 ** 40
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        assert freq_sweep(0.0, 0.0, True, 0.0, 10.0).collect().size == 0
+        with pytest.raises(_lib.SdrGpuError):
+            freq_sweep(np.inf, 1.0, False, 0.0, 10.0)   # +inf samples: refused, not materialised
+
+
 def test_cu8_window_raw_frames_convert_samples(sdr, oracle):
     """window(..).decimate(..).map(f) with a non-FFT map sees Complex samples, as
     RtlTcpSignal::next yields them (src/rtltcp.rs:156-164)."""

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 #include "abi_common.hpp"
 
@@ -80,56 +81,74 @@ int sdrgpu_comm_gather(sdrgpu_comm* c, const void* d_send, void* d_recv, size_t 
 // Uneven blocks (nch % nranks != 0): point-to-point sends from / to the root inside one
 // RCCL group (every link of the root's xGMI fan-out is driven at once); the root's own
 // block is a device-local copy.  bytes / displs: nranks host entries, identical on all ranks.
-int sdrgpu_comm_scatterv(sdrgpu_comm* c, const void* d_send, const size_t* bytes,
-                         const size_t* displs, void* d_recv, int root, void* stream) {
+// sdrgpu_comm_plan_v is the whole decision (which ops, which peers, which offsets); the two
+// collectives only execute its ops, so the CPU suite checks every split through the plan.
+int sdrgpu_comm_plan_v(int nranks, int rank, int root, int gather, const size_t* bytes,
+                       const size_t* displs, sdrgpu_comm_op* ops, int max_ops, int* n_ops) {
+    if (!n_ops || !bytes || nranks < 1 || rank < 0 || rank >= nranks || root < 0 ||
+        root >= nranks || (rank == root && !displs) || (ops && max_ops < 0))
+        return SDRGPU_ERR_INVALID;
+    int n = 0;
+    auto add = [&](int kind, int peer, size_t off, size_t nb) {
+        if (ops && n < max_ops) ops[n] = sdrgpu_comm_op{kind, peer, off, nb};
+        ++n;
+    };
+    if (rank == root) {
+        for (int r = 0; r < nranks; ++r)
+            if (r != root && bytes[r])
+                add(gather ? SDRGPU_COMM_RECV : SDRGPU_COMM_SEND, r, displs[r], bytes[r]);
+        if (bytes[root]) add(SDRGPU_COMM_COPY, root, displs[root], bytes[root]);
+    } else if (bytes[rank]) {
+        add(gather ? SDRGPU_COMM_SEND : SDRGPU_COMM_RECV, root, 0, bytes[rank]);
+    }
+    *n_ops = n;
+    return (ops && n > max_ops) ? SDRGPU_ERR_INVALID : SDRGPU_OK;
+}
+
+// Execute the plan: `root_buf` is the root's packed buffer (d_send of scatterv, d_recv of
+// gatherv), `own` this rank's own block (d_recv of scatterv, d_send of gatherv).
+static int comm_run_v(sdrgpu_comm* c, int gather, const void* root_buf_c, const void* own_c,
+                      const size_t* bytes, const size_t* displs, int root, void* stream) {
     if (!c || !bytes || root < 0 || root >= c->nranks) return SDRGPU_ERR_INVALID;
-    if (c->rank == root && (!d_send || !displs)) return SDRGPU_ERR_INVALID;
-    if (bytes[c->rank] && !d_recv) return SDRGPU_ERR_INVALID;
+    if (c->rank == root && (!root_buf_c || !displs)) return SDRGPU_ERR_INVALID;
+    if (bytes[c->rank] && !own_c) return SDRGPU_ERR_INVALID;
+    char* root_buf = const_cast<char*>(static_cast<const char*>(root_buf_c));
+    char* own = const_cast<char*>(static_cast<const char*>(own_c));
+    int n = 0;
+    int st = sdrgpu_comm_plan_v(c->nranks, c->rank, root, gather, bytes, displs, nullptr, 0, &n);
+    if (st) return st;
+    std::vector<sdrgpu_comm_op> ops(n);
+    if ((st = sdrgpu_comm_plan_v(c->nranks, c->rank, root, gather, bytes, displs, ops.data(), n, &n)))
+        return st;
     DeviceGuard g(c->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const char* src = static_cast<const char*>(d_send);
-    int st = nccl_status(ncclGroupStart());
-    if (st) return st;
-    if (c->rank == root) {
-        for (int r = 0; r < c->nranks; ++r)
-            if (r != root && bytes[r])
-                if ((st = nccl_status(ncclSend(src + displs[r], bytes[r], ncclUint8, r, c->comm, s))))
-                    break;
-    } else if (bytes[c->rank]) {
-        st = nccl_status(ncclRecv(d_recv, bytes[c->rank], ncclUint8, root, c->comm, s));
+    if ((st = nccl_status(ncclGroupStart()))) return st;
+    for (const auto& op : ops) {
+        char* p = c->rank == root ? root_buf + op.offset : own;
+        if (op.kind == SDRGPU_COMM_SEND)
+            st = nccl_status(ncclSend(p, op.bytes, ncclUint8, op.peer, c->comm, s));
+        else if (op.kind == SDRGPU_COMM_RECV)
+            st = nccl_status(ncclRecv(p, op.bytes, ncclUint8, op.peer, c->comm, s));
+        if (st) break;
     }
     const int end = nccl_status(ncclGroupEnd());
     if (st || end) return st ? st : end;
-    if (c->rank == root && bytes[root])
-        SDRGPU_HIP_TRY(hipMemcpyAsync(d_recv, src + displs[root], bytes[root],
-                                      hipMemcpyDeviceToDevice, s));
+    for (const auto& op : ops)
+        if (op.kind == SDRGPU_COMM_COPY)
+            SDRGPU_HIP_TRY(hipMemcpyAsync(gather ? root_buf + op.offset : own,
+                                          gather ? own : root_buf + op.offset, op.bytes,
+                                          hipMemcpyDeviceToDevice, s));
     return SDRGPU_OK;
+}
+
+int sdrgpu_comm_scatterv(sdrgpu_comm* c, const void* d_send, const size_t* bytes,
+                         const size_t* displs, void* d_recv, int root, void* stream) {
+    return comm_run_v(c, 0, d_send, d_recv, bytes, displs, root, stream);
 }
 
 int sdrgpu_comm_gatherv(sdrgpu_comm* c, const void* d_send, void* d_recv, const size_t* bytes,
                         const size_t* displs, int root, void* stream) {
-    if (!c || !bytes || root < 0 || root >= c->nranks) return SDRGPU_ERR_INVALID;
-    if (c->rank == root && (!d_recv || !displs)) return SDRGPU_ERR_INVALID;
-    if (bytes[c->rank] && !d_send) return SDRGPU_ERR_INVALID;
-    DeviceGuard g(c->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    char* dst = static_cast<char*>(d_recv);
-    int st = nccl_status(ncclGroupStart());
-    if (st) return st;
-    if (c->rank == root) {
-        for (int r = 0; r < c->nranks; ++r)
-            if (r != root && bytes[r])
-                if ((st = nccl_status(ncclRecv(dst + displs[r], bytes[r], ncclUint8, r, c->comm, s))))
-                    break;
-    } else if (bytes[c->rank]) {
-        st = nccl_status(ncclSend(d_send, bytes[c->rank], ncclUint8, root, c->comm, s));
-    }
-    const int end = nccl_status(ncclGroupEnd());
-    if (st || end) return st ? st : end;
-    if (c->rank == root && bytes[root])
-        SDRGPU_HIP_TRY(hipMemcpyAsync(dst + displs[root], d_send, bytes[root],
-                                      hipMemcpyDeviceToDevice, s));
-    return SDRGPU_OK;
+    return comm_run_v(c, 1, d_recv, d_send, bytes, displs, root, stream);
 }
 
 int sdrgpu_comm_barrier(sdrgpu_comm* c, void* stream) {

@@ -202,6 +202,8 @@ SIGNATURES = [
     ("sdrgpu_comm_gatherv", c_int, [_H, c_void_p, c_void_p, _PS, _PS, c_int, c_void_p]),
     ("sdrgpu_comm_barrier", c_int, [_H, c_void_p]),
     ("sdrgpu_comm_destroy", None, [_H]),
+    ("sdrgpu_comm_plan_v", c_int, [c_int, c_int, c_int, c_int, _PS, _PS, c_void_p, c_int,
+                                   POINTER(c_int)]),
 ]
 
 _LIB = None

@@ -48,24 +48,29 @@ def deemphasis() -> "_filter.BiquadD":
 
 def receiver(rtl):
     """src/main.rs:48-81 over `rtl` (rtl_tcp bytes at 1.8 Msps): Signal of (n, 2) f32 frames
-    (left, right) at 48 kHz."""
+    (left, right) at 48 kHz.  Like every other stage, the pilot PLL and the de-emphasis bank
+    are built inside the generators, so each iteration of the returned Signal starts from
+    fresh filter state (the reference builds its chain once per run, main.rs:33-81)."""
+    from .signal import Signal
     if rtl.sample_kind != _lib.CU8:
         raise _lib.SdrGpuError(_lib.ERR_INVALID, "fm.receiver: expects rtl_tcp u8 I/Q (CU8)")
     dev = np.float32(DEVIATION)
     fm = rtl.filter(discriminator_design()).map(
         lambda r: np.where(r["locked"], r["value"], np.float32(0.0)).astype(np.float32) / dev)
-    fm = fm.resample_with(_resample.ConverterType.SincFastest, 48000.0 * 3.0)
-    pilot = pilot_design().design(fm.rate())
+    audio = fm.resample_with(_resample.ConverterType.SincFastest, 48000.0 * 3.0)
 
-    def stereo(v):  # main.rs:61-69 with the pilot PLL on the GPU (state carried per block)
-        mono, diff, _ = pilot.stereo(np.asarray(v, np.float32))
-        return np.stack([mono, diff], axis=1)
+    def stereo():  # main.rs:54-69 with the pilot PLL on the GPU (state carried per block)
+        pilot = pilot_design().design(audio.rate())
+        for v in audio.blocks():
+            mono, diff, _ = pilot.stereo(np.asarray(v, np.float32))
+            yield np.stack([mono, diff], axis=1)
 
-    fm = fm.map(stereo).resample(48000.0)
-    bank = deemphasis().design(fm.rate(), sample_kind=_lib.F32, nch=2)
+    md = Signal(audio.rate(), stereo, None).resample(48000.0)
 
-    def out(frames):  # main.rs:75-81
-        md = bank.process(np.ascontiguousarray(np.asarray(frames, np.float32).T))
-        return np.stack([md[0] + md[1], md[0] - md[1]], axis=1)
+    def out():  # main.rs:75-81
+        bank = deemphasis().design(md.rate(), sample_kind=_lib.F32, nch=2)
+        for frames in md.blocks():
+            y = bank.process(np.ascontiguousarray(np.asarray(frames, np.float32).T))
+            yield np.stack([y[0] + y[1], y[0] - y[1]], axis=1)
 
-    return fm.map(out)
+    return Signal(md.rate(), out, None)

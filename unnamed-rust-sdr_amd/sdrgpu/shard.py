@@ -30,6 +30,43 @@ def time_range(n: int, world: int, rank: int, align: int = 1):
     return lo * align, (hi * align if rank < world - 1 else n)
 
 
+SEND, RECV, COPY = 0, 1, 2  # sdrgpu_comm_op kinds (include/sdrgpu.h)
+
+
+class CommOp(ctypes.Structure):
+    """sdrgpu_comm_op: one transfer of a scatterv / gatherv plan."""
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("offset", ctypes.c_size_t), ("bytes", ctypes.c_size_t)]
+
+
+def counts_displs(bytes_per_rank):
+    """(bytes, displs): rank r's block size and its offset in the root's packed buffer
+    (blocks in rank order, as channel_range lays the channels out)."""
+    b = [int(v) for v in bytes_per_rank]
+    return b, [sum(b[:r]) for r in range(len(b))]
+
+
+def _c_counts(bytes_per_rank):
+    b, d = counts_displs(bytes_per_rank)
+    n = len(b)
+    return (ctypes.c_size_t * n)(*b), (ctypes.c_size_t * n)(*d)
+
+
+def plan_v(nranks: int, rank: int, root: int, gather: bool, bytes_per_rank):
+    """The ops sdrgpu_comm_scatterv (gather False) / gatherv (True) issue on `rank`, as
+    (kind, peer, offset in the root's buffer, bytes) tuples -- sdrgpu_comm_plan_v, host-only
+    (no GPU needed), so every split, including zero-byte ranks, is testable on the CPU."""
+    assert len(bytes_per_rank) == nranks
+    b, d = _c_counts(bytes_per_rank)
+    n = ctypes.c_int()
+    check(lib().sdrgpu_comm_plan_v(nranks, rank, root, int(gather), b, d, None, 0,
+                                   ctypes.byref(n)), "sdrgpu_comm_plan_v")
+    ops = (CommOp * max(1, n.value))()
+    check(lib().sdrgpu_comm_plan_v(nranks, rank, root, int(gather), b, d, ops, n.value,
+                                   ctypes.byref(n)), "sdrgpu_comm_plan_v")
+    return [(o.kind, o.peer, o.offset, o.bytes) for o in ops[:n.value]]
+
+
 def unique_id() -> bytes:
     buf = (ctypes.c_char * ID_BYTES)()
     check(lib().sdrgpu_comm_unique_id(buf), "sdrgpu_comm_unique_id")
@@ -54,11 +91,8 @@ class Comm:
               "sdrgpu_comm_gather")
 
     def _counts(self, bytes_per_rank):
-        n = self.nranks
-        assert len(bytes_per_rank) == n
-        b = (ctypes.c_size_t * n)(*bytes_per_rank)
-        d = (ctypes.c_size_t * n)(*[sum(bytes_per_rank[:r]) for r in range(n)])
-        return b, d
+        assert len(bytes_per_rank) == self.nranks
+        return _c_counts(bytes_per_rank)
 
     def scatterv(self, d_send: int, d_recv: int, bytes_per_rank, root: int = 0, stream=None):
         """Uneven blocks: rank r receives bytes_per_rank[r] bytes, packed in rank order in

@@ -349,13 +349,21 @@ def freq(rate: float, f: float, phase: float, n: int, block: int = DEFAULT_BLOCK
     return from_array(rate, _polar_unit(phs), block)
 
 
+USIZE_MAX = (1 << 64) - 1
+
+
 def _as_usize(v) -> int:
     """`v.round() as usize` for an f32 v (FreqSweep::new, sources.rs:133-134): round half away
     from zero, then the saturating cast (negative -> 0).  |v| + 0.5 is formed in f64 -- in
-    f32 it would itself round (2^23 + 1 -> 2^23 + 2, 0.49999997 -> 1)."""
+    f32 it would itself round (2^23 + 1 -> 2^23 + 2, 0.49999997 -> 1).  Rust's float -> int
+    `as` saturates: NaN and negatives give 0 (e.g. freq_sweep with df = 0 and rate = 0, where
+    inf * 0 = NaN: an empty sweep), +inf gives usize::MAX."""
     v = float(np.float32(v))
-    r = math.floor(abs(v) + 0.5)
-    return int(r) if v > 0 else 0
+    if not v > 0:           # NaN, -0, 0 and negatives
+        return 0
+    if math.isinf(v):
+        return USIZE_MAX
+    return min(int(math.floor(v + 0.5)), USIZE_MAX)
 
 
 def freq_sweep(rate: float, df: float, warmup: bool, start: float, end: float,
@@ -377,6 +385,8 @@ def freq_sweep(rate: float, df: float, warmup: bool, start: float, end: float,
     fstart = as_usize(f32(warmupt * rate32))
     fend = as_usize(f32(fend_t * rate32))
     n = fend
+    if n == USIZE_MAX:  # an unbounded sweep (Rust's lazy iterator would never end)
+        raise _lib.SdrGpuError(_lib.ERR_INVALID, "freq_sweep: unbounded length (+inf samples)")
     dt = f32(1.0) / rate32
     fr = f32(start)
     nph = f32(0.0) / two_pi
