@@ -92,3 +92,56 @@ def test_d1_fir_drop_in_keeps_output_a():
     assert m and m.group(1) == "A"
     # the decimating form is the one whose per-sample output is Option<A>
     assert re.search(r"Filter<A> for GpuFirDecim<A> \{\s*type Output = Option<A>;", src)
+
+
+RUST_SIZE_ALIGN = {"c_int": 4, "i32": 4, "u32": 4, "u8": 1, "usize": 8, "f32": 4, "f64": 8,
+                   "c_long": 8, "c_char": 1}
+
+
+def rust_structs():
+    src = open(SYS).read()
+    out = {}
+    for m in re.finditer(r"#\[repr\(C\)\]\s*#\[derive[^\]]*\]\s*pub struct (\w+) \{(.*?)\}", src,
+                         flags=re.S):
+        out[m.group(1)] = re.findall(r"pub (\w+): ([^,]+),", m.group(2))
+    return out
+
+
+def repr_c_layout(name, structs):
+    """(size, align, {field: offset}) of a #[repr(C)] struct from its Rust field types, by the
+    C layout rules repr(C) follows (x86-64: pointers and c_long are 8 bytes)."""
+    off, align, offs = 0, 1, {}
+    for fname, ftype in structs[name]:
+        ftype = ftype.strip()
+        if ftype.startswith("*"):
+            sz = al = 8
+        elif ftype in RUST_SIZE_ALIGN:
+            sz = al = RUST_SIZE_ALIGN[ftype]
+        else:
+            sz, al, _ = repr_c_layout(ftype, structs)
+        off = (off + al - 1) // al * al
+        offs[fname] = off
+        off += sz
+        align = max(align, al)
+    return (off + align - 1) // align * align, align, offs
+
+
+def test_sys_struct_layouts_match_the_c_header():
+    """Advisor finding r3: the #[repr(C)] structs' field order and Rust types must lay out as
+    the C compiler lays out include/sdrgpu.h's structs.  lib.rs carries the gcc-measured
+    sizes / offsets as compile-time asserts (generated, and checked current above); here the
+    layout implied by the Rust field types is computed independently and compared with them,
+    and the field order with the header's."""
+    src = open(SYS).read()
+    structs = rust_structs()
+    assert set(structs) >= {"sdrgpu_pll_params", "sdrgpu_biquad_design", "sdrgpu_src_data",
+                            "sdrgpu_comm_op"}
+    sizes = dict(re.findall(r"size_of::<(\w+)>\(\) == (\d+)\)", src))
+    offsets = re.findall(r"offset_of!\((\w+), (\w+)\) == (\d+)\)", src)
+    assert set(sizes) == set(structs)
+    for name in structs:
+        size, _, offs = repr_c_layout(name, structs)
+        assert size == int(sizes[name]), (name, size, sizes[name])
+        c_offs = [(f, int(o)) for s, f, o in offsets if s == name]
+        assert [f for f, _ in c_offs] == [f for f, _ in structs[name]], name   # same order
+        assert all(offs[f] == o for f, o in c_offs), (name, offs, c_offs)

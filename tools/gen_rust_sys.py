@@ -102,6 +102,33 @@ def parse(src):
 RUST_KEYWORDS = {"in", "type", "ref", "mod", "fn", "impl", "loop", "move", "self", "use"}
 
 
+def c_layouts(structs):
+    """{struct: (sizeof, [(field, offsetof), ...])} as gcc lays the header's structs out on
+    this ABI (x86-64 Linux, the reference's target): a probe including sdrgpu.h is compiled
+    and run.  The generated crate asserts the same numbers at compile time."""
+    import tempfile
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "sdrgpu.h"', "int main(void) {"]
+    for sname, fields in structs:
+        lines.append(f'    printf("S {sname} %zu\\n", sizeof({sname}));')
+        for fname, _ in fields:
+            lines.append(f'    printf("F {sname} {fname} %zu\\n", offsetof({sname}, {fname}));')
+    lines += ["    return 0;", "}"]
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "probe.c"), os.path.join(d, "probe")
+        open(src, "w").write("\n".join(lines) + "\n")
+        import subprocess
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    lay = {}
+    for line in out.splitlines():
+        t = line.split()
+        if t[0] == "S":
+            lay[t[1]] = (int(t[2]), [])
+        else:
+            lay[t[1]][1].append((t[2], int(t[3])))
+    return lay
+
+
 def generate():
     funcs, enums, defines, structs, opaque = parse(open(HEADER).read())
     L = ["// GENERATED by tools/gen_rust_sys.py from include/sdrgpu.h -- do not edit by hand.",
@@ -134,6 +161,15 @@ def generate():
             L.append(f"    pub {fname}: {rust_type(ftype)},")
         L.append("}")
         L.append("")
+    lay = c_layouts(structs)
+    L.append("// #[repr(C)] layouts = the C compiler's (sizes / offsets from tools/gen_rust_sys.py's")
+    L.append("// gcc probe of include/sdrgpu.h): a field-order or type mismatch fails to compile.")
+    for sname, _ in structs:
+        size, offs = lay[sname]
+        L.append(f"const _: () = assert!(std::mem::size_of::<{sname}>() == {size});")
+        for fname, off in offs:
+            L.append(f"const _: () = assert!(std::mem::offset_of!({sname}, {fname}) == {off});")
+    L.append("")
     L.append('#[link(name = "sdrgpu")]')
     L.append('extern "C" {')
     for name, ret, params in funcs:
