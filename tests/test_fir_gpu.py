@@ -284,12 +284,38 @@ def test_fir_full_size_c2_properties(sdr, oracle):
         assert np.array_equal(y2, 2 * y1)
 
 
+def mxh_d4_c64_dealing(n_out, cus=256):
+    """Host mirror of fir_mxh_launch's c64 D = 4 dealing (fir_mxh.hip:624-637): tiles of 256
+    kept outputs, units (runs) of kRunTiles = 2 tiles, unit u dealt grid-strided to wave
+    u mod nwaves (a wave walks units w, w + nwaves, ... as one pipeline)."""
+    tpc = -(-n_out // 256)
+    seg = min(2, tpc)
+    units = -(-tpc // seg)
+    nwaves = 8 * min(cus, -(-units // 8))
+    return {"tiles": tpc, "units": units, "nwaves": nwaves,
+            "last_unit_tiles": tpc - (units - 1) * seg,
+            "last_tile_outputs": n_out - (tpc - 1) * 256,
+            "last_unit_wave": (units - 1) % nwaves,
+            "min_units_per_wave": units // nwaves}
+
+
 def test_fir_mx_run_boundaries_whole_stream(sdr, oracle):
-    """The D = 4 kernel deals runs of 8 tiles to each CU's waves and walks a wave's runs as
-    one pipeline (a run's first window re-reads the 256 samples before it).  At 2^25 + a
-    ragged tail every wave owns two or more runs, so run starts, the cross-run prefetch and
-    the partial last tile all occur; the WHOLE output is compared with the oracle, in two
-    device blocks whose cut is not tile-aligned."""
+    """The c64 D = 4 kernel deals runs of 2 tiles (512 kept outputs) grid-strided and walks a
+    wave's runs as one pipeline: each run's first window re-reads the 256 samples before it
+    (fir_mxh.hip:410, :472) and the raw-tile prefetch crosses into the wave's next run.  Two
+    device blocks, cut mid-tile (not tile- or run-aligned), carry the history between calls:
+      block 1 (1,234,567 outputs): 4823 tiles in 2412 units over 2048 waves -- waves 0-363 own
+        two units, and wave 363's second and last unit is ONE partial tile of 135 outputs;
+      block 2 (7,154,818 outputs): 27,949 tiles in 13,975 units -- every wave walks >= 6 units
+        (6 cross-unit history reloads and prefetches), and the last unit (wave 1686's
+        seventh) is again one partial tile (130 outputs).
+    (Arithmetic for 256 CUs, checked below through the host mirror of the dealing.)  The
+    WHOLE output is compared with the oracle."""
+    b1, b2 = mxh_d4_c64_dealing(1234567), mxh_d4_c64_dealing(7154818)
+    assert (b1["units"], b1["nwaves"], b1["last_unit_tiles"], b1["last_tile_outputs"],
+            b1["last_unit_wave"]) == (2412, 2048, 1, 135, 363)
+    assert b2["min_units_per_wave"] >= 6 and b2["last_unit_tiles"] == 1
+    assert (b2["last_tile_outputs"], b2["last_unit_wave"]) == (130, 1686)
     from sdrgpu.device import DeviceBuffer
     import scipy.signal as ss
     n = (1 << 25) + 4 * 777 + 3
@@ -306,7 +332,7 @@ def test_fir_mx_run_boundaries_whole_stream(sdr, oracle):
     m1 = f.process_dev(dx.ptr, cut, dy.ptr, n_out + 8)
     m2 = f.process_dev(dx.ptr + 8 * cut, n - cut, dy.ptr + 8 * m1, n_out + 8 - m1)
     f.sync()
-    assert m1 + m2 == n_out
+    assert (m1, m2) == (1234567, 7154818) and m1 + m2 == n_out
     ref = oracle.fir_batch(taps, x[None, :], D, nthreads=16)[0]
     assert_parity(dy.download(n_out), ref, what="2^25 stream, two blocks")
 
