@@ -29,6 +29,10 @@ p = sys.argv[1]; s = open(p).read()
 old = "const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;"
 assert old in s
 s = s.replace(old, "const float2* src2 = p.dummy;")
+old = """            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch * (p.ld_in / 2) + (j2 >> 1)
+                                          : reinterpret_cast<const unsigned*>(p.dummy);"""
+assert old in s  # the rtl_tcp u8 launch's tile loads too
+s = s.replace(old, "            const unsigned* src2u = reinterpret_cast<const unsigned*>(p.dummy);")
 open(p, 'w').write(s)
 PY
   elif [ $v = prio ]; then  # static s_setprio 1 for the younger half (waves 4-7) of the workgroup
