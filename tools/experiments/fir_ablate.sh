@@ -167,6 +167,27 @@ s = s.replace(old2, """    __syncthreads();
 """ + old2, 1)
 open(p, 'w').write(s)
 PY
+  elif [ $v = clk ]; then  # per-workgroup shader-clock / 100 MHz ticks over the launch, 16 B per workgroup at out - 4 KiB (timing-only: the caller reserves that space)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    const int lane = threadIdx.x & 63;"
+assert old in s
+s = s.replace(old, "    const unsigned long long c_wg0 = __builtin_readcyclecounter();\n"
+                   "    const unsigned long long t_wg0 = __builtin_amdgcn_s_memrealtime();\n" + old, 1)
+old2 = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
+assert old2 in s
+s = s.replace(old2, """    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long c_end = __builtin_readcyclecounter();
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* o = reinterpret_cast<unsigned long long*>(p.out) - 512 + 2 * (blockIdx.x & 255);
+        o[0] = t_end - t_wg0;
+        o[1] = c_end - c_wg0;
+    }
+""" + old2, 1)
+open(p, 'w').write(s)
+PY
   elif [ $v = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys
