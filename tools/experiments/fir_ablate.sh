@@ -9,9 +9,10 @@ mkdir -p tools/experiments/abl
 make -C unnamed-rust-sdr_amd -s
 OBJS=$(ls unnamed-rust-sdr_amd/build/*.o | grep -v fir_mxh.o)
 for v in ${VARIANTS:-nomfma noload}; do
-  src=tools/experiments/abl/fir_mxh_$v.hip
+  src=tools/experiments/abl/fir_mxh_$v.hip  # (v may be composite, e.g. clk+nomfma)
   cp unnamed-rust-sdr_amd/csrc/fir_mxh.hip $src
-  if [ $v = nomfma ]; then
+  for part in ${v//+/ }; do  # composite variants: a+b applies a, then b
+  if [ $part = nomfma ]; then
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -22,7 +23,7 @@ s = s.replace(old, """    c[0] += __uint_as_float(b[0] & 0x3ffu);
     return c;""")
 open(p, 'w').write(s)
 PY
-  elif [ $v = noload ]; then
+  elif [ $part = noload ]; then
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -35,7 +36,7 @@ assert old in s  # the rtl_tcp u8 launch's tile loads too
 s = s.replace(old, "            const unsigned* src2u = reinterpret_cast<const unsigned*>(p.dummy);")
 open(p, 'w').write(s)
 PY
-  elif [ $v = prio ]; then  # static s_setprio 1 for the younger half (waves 4-7) of the workgroup
+  elif [ $part = prio ]; then  # static s_setprio 1 for the younger half (waves 4-7) of the workgroup
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -44,7 +45,7 @@ assert old in s
 s = s.replace(old, old + "\n    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);")
 open(p, 'w').write(s)
 PY
-  elif [ $v = stplain ]; then  # plain (temporal) output stores instead of non-temporal
+  elif [ $part = stplain ]; then  # plain (temporal) output stores instead of non-temporal
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -55,7 +56,7 @@ s = s.replace(old, """                    o4[0] = y0;
                     o4[1] = y1;""")
 open(p, 'w').write(s)
 PY
-  elif [ $v = ldplain ]; then  # plain loads for the streamed tiles instead of non-temporal
+  elif [ $part = ldplain ]; then  # plain loads for the streamed tiles instead of non-temporal
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -65,7 +66,7 @@ assert old in s
 s = s.replace(old, """                        const f32x4 r = *reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane);""")
 open(p, 'w').write(s)
 PY
-  elif [ $v = wvdiv ]; then  # wave index left divergent (VGPR cursor math, no SGPR spills)
+  elif [ $part = wvdiv ]; then  # wave index left divergent (VGPR cursor math, no SGPR spills)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -74,7 +75,7 @@ assert old in s
 s = s.replace(old, "const int wv = threadIdx.x >> 6;")
 open(p, 'w').write(s)
 PY
-  elif [ $v = nohist ]; then  # history groups not re-staged per window (wrong outputs: cost probe)
+  elif [ $part = nohist ]; then  # history groups not re-staged per window (wrong outputs: cost probe)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -83,7 +84,7 @@ assert old in s
 s = s.replace(old, "                    for (int k = 0; k < NH; ++k) if (scn == 0.f) put(WN + hist_addr(k), hr[k], scn);")
 open(p, 'w').write(s)
 PY
-  elif [ $v = nosplit ]; then  # hi plane only, lo = 0 (wrong precision: split-VALU cost probe)
+  elif [ $part = nosplit ]; then  # hi plane only, lo = 0 (wrong precision: split-VALU cost probe)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -92,7 +93,7 @@ assert old in s
 s = s.replace(old, "    lo = 0u;")
 open(p, 'w').write(s)
 PY
-  elif [ $v = nomax ]; then  # fixed window scale (no abs-max / wave reduction: cost probe)
+  elif [ $part = nomax ]; then  # fixed window scale (no abs-max / wave reduction: cost probe)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -101,7 +102,7 @@ assert old in s
 s = s.replace(old, "            return 15;")
 open(p, 'w').write(s)
 PY
-  elif [ $v = early ]; then  # stage all of tile k+1 and issue all of tile k+2's loads BEFORE tile k's MFMAs
+  elif [ $part = early ]; then  # stage all of tile k+1 and issue all of tile k+2's loads BEFORE tile k's MFMAs
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -134,7 +135,7 @@ i1 = s.index("            }\n            if (!ld_run) {", i0)
 s = s[:i0] + s[i1:]
 open(p, 'w').write(s)
 PY
-  elif [ $v = mfma4 ]; then  # the two taps-hi x samples-lo MFMAs dropped (4 of 6 per chunk; wrong precision: MFMA-count probe)
+  elif [ $part = mfma4 ]; then  # the two taps-hi x samples-lo MFMAs dropped (4 of 6 per chunk; wrong precision: MFMA-count probe)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -146,7 +147,7 @@ assert old in s
 s = s.replace(old, "")
 open(p, 'w').write(s)
 PY
-  elif [ $v = wgtime ]; then  # per-workgroup start/end s_memrealtime (100 MHz) into out[0..511]: tail census
+  elif [ $part = wgtime ]; then  # per-workgroup start/end s_memrealtime (100 MHz) into out[0..511]: tail census
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -167,7 +168,7 @@ s = s.replace(old2, """    __syncthreads();
 """ + old2, 1)
 open(p, 'w').write(s)
 PY
-  elif [ $v = clk ]; then  # per-workgroup shader-clock / 100 MHz ticks over the launch, 16 B per workgroup at out - 4 KiB (timing-only: the caller reserves that space)
+  elif [ $part = clk ]; then  # per-workgroup shader-clock / 100 MHz ticks over the launch, 16 B per workgroup at out - 4 KiB (timing-only: the caller reserves that space)
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -188,7 +189,7 @@ s = s.replace(old2, """    __syncthreads();
 """ + old2, 1)
 open(p, 'w').write(s)
 PY
-  elif [ $v = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
+  elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -199,7 +200,7 @@ for old, new in (("constexpr int kWaves = 8;               // two waves per SIMD
     s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
-  elif [ $v = mfma16 ]; then  # each 16x16x32 MFMA as two 16x16x16 ones over the two K halves of the same fragments
+  elif [ $part = mfma16 ]; then  # each 16x16x32 MFMA as two 16x16x16 ones over the two K halves of the same fragments
     python3 - $src <<'PY'
 import sys
 p = sys.argv[1]; s = open(p).read()
@@ -214,8 +215,8 @@ s = s.replace(old, """    typedef _Float16 f16x4 __attribute__((ext_vector_type(
     return __builtin_amdgcn_mfma_f32_16x16x16f16(ahi, bhi, c, 0, 0, 0);""")
 open(p, 'w').write(s)
 PY
-  elif [ $v = lomask2 ] || [ $v = lomask3 ]; then  # low mantissa bits of the lo planes cleared (MFMA switching energy)
-    python3 - $src $v <<'PY'
+  elif [ $part = lomask2 ] || [ $part = lomask3 ]; then  # low mantissa bits of the lo planes cleared (MFMA switching energy)
+    python3 - $src $part <<'PY'
 import sys
 p, v = sys.argv[1], sys.argv[2]; s = open(p).read()
 m = {'lomask2': '0xFFFCFFFCu', 'lomask3': '0xFFF8FFF8u'}[v]
@@ -227,8 +228,8 @@ assert old2 in s
 s = s.replace(old2, "                al[c][jj] = lw & " + m + ";")
 open(p, 'w').write(s)
 PY
-  elif [ $v = mfmaord ] || [ $v = dualacc ]; then  # MFMA operand order (switching energy)
-    python3 - $src $v <<'PY'
+  elif [ $part = mfmaord ] || [ $part = dualacc ]; then  # MFMA operand order (switching energy)
+    python3 - $src $part <<'PY'
 import sys
 p, v = sys.argv[1], sys.argv[2]; s = open(p).read()
 old = """                    cr[j] = mfma(al[c], f[0], cr[j]);
@@ -279,6 +280,7 @@ s = s.replace(old, new)
 open(p, 'w').write(s)
 PY
   fi
+  done
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip -c $src -o tools/experiments/abl/fir_mxh_$v.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/experiments/abl/lib_$v.so $OBJS tools/experiments/abl/fir_mxh_$v.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 done
