@@ -216,7 +216,9 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // 2 MFMAs per component per chunk.
 // D: decimation 4 (XOR-swizzled LDS rows, block map sigma) or 1 (linear LDS: blocks 16
 // samples apart already hit distinct banks; identity block map).
-template <int NCH, bool U8 = false, int D = 4, int CS = 1>
+// ONE: a single channel dealt grid-strided (the headline shape): cursors are 32-bit unit /
+// tile indices with no channel arithmetic (no 64-bit division per unit, no SGPR spills).
+template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
@@ -288,19 +290,28 @@ void fir_mxh_kernel(MxhParams p) {
     // computed and stored, k+1 staged, k+2 loading) advance together, so the raw-tile
     // prefetch crosses run boundaries; a run's first window re-reads the H samples before it
     // (issued one tile ahead, into the history registers).
+    using Idx = std::conditional_t<ONE, int, long>;
     struct Cur {
-        long u, t, ch, tu, nt;
+        Idx u, t, tu, nt;
+        long ch_;
         bool ok;
+        __device__ long ch() const { return ONE ? 0L : ch_; }
     };
-    const long ust = p.blocked ? (long)kWaves : nwaves;
-    const long ub1 = p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units;
-    auto seek = [&](Cur& c, long u) {
+    const Idx ust = ONE ? (Idx)nwaves : (p.blocked ? (long)kWaves : nwaves);
+    const Idx ub1 = ONE ? (Idx)p.units : (p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units);
+    auto seek = [&](Cur& c, Idx u) {
         c.u = u;
         c.t = 0;
         c.ok = u < ub1;
-        c.ch = c.ok ? u / p.spc : 0;
-        c.tu = (u - c.ch * p.spc) * p.seg_tiles;
-        c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        if constexpr (ONE) {
+            c.ch_ = 0;
+            c.tu = u * (Idx)p.seg_tiles;
+            c.nt = c.ok ? std::min((Idx)p.seg_tiles, (Idx)p.tpc - c.tu) : 0;
+        } else {
+            c.ch_ = c.ok ? u / p.spc : 0;
+            c.tu = (u - c.ch_ * p.spc) * p.seg_tiles;
+            c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        }
         if (c.ok && c.nt <= 0) c.ok = false;  // (units past a channel's last tile: none by construction)
     };
     auto adv = [&](Cur& c) {
@@ -311,12 +322,12 @@ void fir_mxh_kernel(MxhParams p) {
     auto tile_j0 = [&](const Cur& c) { return (long)TI * (c.tu + c.t); };
     auto tile_fast = [&](const Cur& c) { return (long)TI * (c.tu + c.t + 1) <= n_in; };
     auto fetch = [&](const Cur& c, long j) -> Raw {
-        const float2* hist = p.hist + c.ch * (long)(K - 1);
+        const float2* hist = p.hist + c.ch() * (long)(K - 1);
         if constexpr (U8)
-            return fetch_pair_u8(reinterpret_cast<const unsigned short*>(p.in_u8) + c.ch * p.ld_in, hist, j,
+            return fetch_pair_u8(reinterpret_cast<const unsigned short*>(p.in_u8) + c.ch() * p.ld_in, hist, j,
                                  n_in, K);
         else
-            return fetch_pair(p.in + c.ch * p.ld_in, hist, j, n_in, K);
+            return fetch_pair(p.in + c.ch() * p.ld_in, hist, j, n_in, K);
     };
     auto put = [&](int a, const Raw& w, float sc) {
         if constexpr (U8) put_pair_u8<PLB>(smem, a, w);
@@ -326,10 +337,10 @@ void fir_mxh_kernel(MxhParams p) {
     auto ldx = [&](const Cur& c, long j, auto nt_c) -> Raw {
         constexpr bool NT = decltype(nt_c)::value;
         if constexpr (U8) {
-            const unsigned* q = p.in_u8 + c.ch * (p.ld_in / 2) + (j >> 1);
+            const unsigned* q = p.in_u8 + c.ch() * (p.ld_in / 2) + (j >> 1);
             return NT ? __builtin_nontemporal_load(q) : *q;
         } else {
-            const f32x4* q = reinterpret_cast<const f32x4*>(p.in + c.ch * p.ld_in + j);
+            const f32x4* q = reinterpret_cast<const f32x4*>(p.in + c.ch() * p.ld_in + j);
             const f32x4 r = NT ? __builtin_nontemporal_load(q) : *q;
             return make_float4(r[0], r[1], r[2], r[3]);
         }
@@ -392,7 +403,7 @@ void fir_mxh_kernel(MxhParams p) {
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
     Cur cm, st, ld;
-    seek(cm, p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave);
+    seek(cm, ONE ? (Idx)wave : (p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave));
     if (cm.ok) {
         Raw nx[NG], hr[NH];
         load_hist(hr, cm);
@@ -420,8 +431,8 @@ void fir_mxh_kernel(MxhParams p) {
             const bool ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
             // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
             const long j2 = tile_j0(ld);
-            const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;
-            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch * (p.ld_in / 2) + (j2 >> 1)
+            const float2* src2 = fast2 ? p.in + ld.ch() * p.ld_in + j2 : p.dummy;
+            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch() * (p.ld_in / 2) + (j2 >> 1)
                                           : reinterpret_cast<const unsigned*>(p.dummy);
             const int s_next = window_scale(nx, hr);
             const float scn = exp2i(s_next);
@@ -493,8 +504,8 @@ void fir_mxh_kernel(MxhParams p) {
             }
             if (!fast2 && ld.ok) load_tile(nx, ld);
             const int so = -(s_cur + p.sh);
-            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            const long m0 = (cm.tu + cm.t) * G::TO;
+            float2* __restrict__ out = p.out + cm.ch() * p.ld_out;
+            const long m0 = (long)(cm.tu + cm.t) * G::TO;
 #pragma unroll
             for (int j = 0; j < CS; ++j) {
                 const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
@@ -635,19 +646,23 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     p.units = nch * p.spc;
     p.blocked = run > 0 && u8;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
-#define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
+    // one channel dealt grid-strided with 32-bit unit indices: the ONE instantiation
+    const bool one = !u8 && D == 4 && nch == 1 && !p.blocked && p.units < (1L << 30) &&
+                     p.tpc < (1L << 30);
+#define SDRGPU_MXH_GO(CC, U, DD, CS, ONE)                                                      \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE>), dim3(blocks), dim3(kBlock),       \
                        (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
-        if (u8) SDRGPU_MXH_GO(CC, true, 4, 1);                                                 \
-        else SDRGPU_MXH_GO(CC, false, 4, 1);                                                   \
+        if (u8) SDRGPU_MXH_GO(CC, true, 4, 1, false);                                          \
+        else if (one) SDRGPU_MXH_GO(CC, false, 4, 1, true);                                    \
+        else SDRGPU_MXH_GO(CC, false, 4, 1, false);                                            \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
 #define SDRGPU_MXH_CASE1(CC)                                                                   \
     if (D == 1 && NCH == CC) {                                                                 \
-        SDRGPU_MXH_GO(CC, false, 1, kCs1);                                                     \
+        SDRGPU_MXH_GO(CC, false, 1, kCs1, false);                                              \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
