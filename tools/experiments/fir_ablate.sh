@@ -189,6 +189,58 @@ s = s.replace(old2, """    __syncthreads();
 """ + old2, 1)
 open(p, 'w').write(s)
 PY
+  elif [ $part = mprio ]; then  # priority 1 while a wave issues each chunk's MFMAs, 0 for its staging (no static per-wave priority)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);"
+assert old in s
+s = s.replace(old, "")
+old = """                    __builtin_amdgcn_sched_barrier(0);
+                    const u32x4(&f)[4] = fb["""
+assert old in s
+s = s.replace(old, """                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_s_setprio(1);
+                    const u32x4(&f)[4] = fb[""")
+old = """                    cr[j] = mfma(ah[c], f[0], cr[j]);
+                    ci[j] = mfma(ah[c], f[2], ci[j]);
+                }"""
+assert old in s
+s = s.replace(old, """                    cr[j] = mfma(ah[c], f[0], cr[j]);
+                    ci[j] = mfma(ah[c], f[2], ci[j]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_s_setprio(0);
+                }""")
+open(p, 'w').write(s)
+PY
+  elif [ $part = frag2 ]; then  # B fragments read two chunks ahead (three slots) when no fragment is shared (D = 4)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "            u32x4 fb[2][4];"
+assert old in s
+s = s.replace(old, "            u32x4 fb[3][4];")
+old = """            read_frags(fb[0], 0, 0);
+            // D = 1"""
+assert old in s
+s = s.replace(old, """            read_frags(fb[0], 0, 0);
+            if (D == 4 && CS * NCH > 1) read_frags(fb[1], 1, 0);
+            // D = 1""")
+old = """                    const int ni = i + 1;
+                    const bool reuse = kShare && ni % NCH == 0;
+                    if (ni < CS * NCH && !reuse)
+                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], ni % NCH, ni / NCH);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const u32x4(&f)[4] = fb[(kShare ? i - j : i) & 1];"""
+assert old in s
+s = s.replace(old, """                    const int ni = i + (D == 4 ? 2 : 1);
+                    const bool reuse = kShare && ni % NCH == 0;
+                    if (ni < CS * NCH && !reuse)
+                        read_frags(fb[D == 4 ? ni % 3 : (kShare ? ni - ni / NCH : ni) & 1], ni % NCH, ni / NCH);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const u32x4(&f)[4] = fb[D == 4 ? i % 3 : (kShare ? i - j : i) & 1];""")
+open(p, 'w').write(s)
+PY
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys
