@@ -6,12 +6,15 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r04_var}
 mkdir -p $O
 cd $R
-MAKEFLAGS=-j16 VARIANTS="$VARIANTS" timeout -k 10 600 bash tools/experiments/fir_ablate.sh > $O/build.log 2>&1 || { tail -20 $O/build.log; exit 1; }
+BUILD=$(echo $VARIANTS | tr " " "\n" | grep -v "^base$" | tr "\n" " ")
+[ -z "$BUILD" ] || MAKEFLAGS=-j16 VARIANTS="$BUILD" timeout -k 10 600 bash tools/experiments/fir_ablate.sh > $O/build.log 2>&1 || { tail -20 $O/build.log; exit 1; }
 for rep in $(seq 1 ${REPS:-3}); do
   for v in prod $VARIANTS; do
     for kind in ${KINDS:-c64}; do
       f=$O/${v}_${kind}_$rep
-      if [ $v = prod ]; then
+      if [ $v = base ]; then
+        timeout -k 10 120 python -u tools/experiments/run_with_lib.py tools/experiments/ab/lib_base.so tools/gpu/r04_series.py --kind $kind --long 200 > $f.jsonl 2> $f.err || { tail -20 $f.err; exit 2; }
+      elif [ $v = prod ]; then
         timeout -k 10 120 python -u tools/gpu/r04_series.py --kind $kind --long 200 > $f.jsonl 2> $f.err || { tail -20 $f.err; exit 2; }
       else
         timeout -k 10 120 python -u tools/experiments/run_with_lib.py tools/experiments/abl/lib_$v.so tools/gpu/r04_series.py --kind $kind --long 200 > $f.jsonl 2> $f.err || { tail -20 $f.err; exit 2; }

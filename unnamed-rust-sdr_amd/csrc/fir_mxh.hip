@@ -218,7 +218,7 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // samples apart already hit distinct banks; identity block map).
 // ONE: a single channel dealt grid-strided (the headline shape): cursors are 32-bit unit /
 // tile indices with no channel arithmetic (no 64-bit division per unit, no SGPR spills).
-template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false>
+template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false, bool STAG = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
@@ -233,7 +233,7 @@ void fir_mxh_kernel(MxhParams p) {
     // the younger half of the workgroup (waves 4-7) loses VALU arbitration to its SIMD partner
     // on every segment (priority, then age): one static s_setprio 1 for it, no per-segment
     // flips (configs[1]: 0.5229 -> 0.5189 ms over 3 A/B reps, profiles/r02_fir_prio_ab.txt)
-    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
+    if (!STAG && wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
     const long wave = (long)blockIdx.x * kWaves + wv;
     const long nwaves = (long)gridDim.x * kWaves;
     const int g = lane >> 4, v = lane & 15;
@@ -402,13 +402,15 @@ void fir_mxh_kernel(MxhParams p) {
 
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
-    Cur cm, st, ld;
+    static_assert(!STAG || ONE, "staggered phases: single-channel dealing");
+    Cur cm{}, st{}, ld{};
     seek(cm, ONE ? (Idx)wave : (p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave));
+    Raw nx[NG], hr[NH];
+    int s_cur = 0;
     if (cm.ok) {
-        Raw nx[NG], hr[NH];
         load_hist(hr, cm);
         load_tile(nx, cm);
-        int s_cur = window_scale(nx, hr);
+        s_cur = window_scale(nx, hr);
         {
             const float sc = exp2i(s_cur);
 #pragma unroll
@@ -423,21 +425,130 @@ void fir_mxh_kernel(MxhParams p) {
         if (st.ok) load_tile(nx, st);
         ld = st;
         adv(ld);
+    }
 
+    constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
+    constexpr int NKO = NG > NH ? NG - NH : 0;
+    // column set j of the tile reads 256 samples (D = 1) further into the window
+    auto read_frags = [&](u32x4 (&f)[4], int tau, int c, int j) {
+        const int a = rb[c] + tau * WINB + j * 2 * 256 * D;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (!U8 || (q & 1) == 0)
+                f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
+    };
+    // D = 1: column set j + 1's chunk 0 reads the window span of set j's last chunk
+    // (256 samples = NCH - 1 chunks of 32 further), so that fragment is not re-read:
+    // the slot of chunk i is (i - j) & 1
+    constexpr bool kShare = D == 1 && 32 * (NCH - 1) == 256;
+    // chunk i's MFMAs on fragment slot f
+    auto mfma_chunk = [&](f32x4 (&cr)[CS], f32x4 (&ci)[CS], const u32x4 (&f)[4], int i) {
+        const int j = i / NCH, c = i % NCH;
+        cr[j] = mfma(al[c], f[0], cr[j]);
+        ci[j] = mfma(al[c], f[2], ci[j]);
+        if (!U8) {
+            cr[j] = mfma(ah[c], f[1], cr[j]);
+            ci[j] = mfma(ah[c], f[3], ci[j]);
+        }
+        cr[j] = mfma(ah[c], f[0], cr[j]);
+        ci[j] = mfma(ah[c], f[2], ci[j]);
+    };
+    // tile c's outputs (accumulators scaled back by 2^-(s + sh)) to HBM
+    auto store_out = [&](const f32x4 (&cr)[CS], const f32x4 (&ci)[CS], const Cur& c, int s) {
+        const int so = -(s + p.sh);
+        float2* __restrict__ out = p.out + c.ch() * p.ld_out;
+        const long m0 = (long)(c.tu + c.t) * G::TO;
+#pragma unroll
+        for (int j = 0; j < CS; ++j) {
+            const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
+            float yr[4], yi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
+                yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
+            }
+            if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
+                // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
+                // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
+                // line) and the second those of the odd-v blocks (steady-state probe: 0.472
+                // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
+                const bool ev = (v & 1) == 0;
+                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                f32x4 rx;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
+                        __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
+                const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
+                f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
+                f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
+                __builtin_nontemporal_store(ev ? y0 : rx, o4);
+                __builtin_nontemporal_store(ev ? rx : y1, p4);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+            }
+        }
+    };
+    // staging of tile st into the window buffer at byte offset wn (its history groups first,
+    // then each new group k, whose registers then take group k of tile ld: the prefetch);
+    // stage_group(k) runs after chunk k's MFMAs in the interleaved body, all at once in the
+    // staggered one
+    struct Stage {
+        bool fast2, ld_run;
+        const float2* src2;
+        const unsigned* src2u;
+        int s_next;
+        float scn;
+        Raw keep[NK];
+    };
+    auto stage_begin = [&](Stage& S) {
+        S.fast2 = ld.ok && tile_fast(ld);
+        S.ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
+        // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
+        const long j2 = tile_j0(ld);
+        S.src2 = S.fast2 ? p.in + ld.ch() * p.ld_in + j2 : p.dummy;
+        S.src2u = S.fast2 ? p.in_u8 + ld.ch() * (p.ld_in / 2) + (j2 >> 1)
+                          : reinterpret_cast<const unsigned*>(p.dummy);
+        S.s_next = window_scale(nx, hr);
+        S.scn = exp2i(S.s_next);
+    };
+    auto stage_hist = [&](Stage& S, int wn) {  // window k+1's history (old hr); then tile k+2's
+#pragma unroll
+        for (int k = 0; k < NH; ++k) put(wn + hist_addr(k), hr[k], S.scn);
+        if (S.ld_run) load_hist(hr, ld);
+    };
+    auto stage_group = [&](Stage& S, int wn, int k) {
+        put(wn + new_addr(k), nx[k], S.scn);
+        if (k >= NG - NH) S.keep[k - NKO] = nx[k];
+        if constexpr (U8) {
+            nx[k] = __builtin_nontemporal_load(S.src2u + 64 * k + lane);
+        } else {
+            const f32x4 r = __builtin_nontemporal_load(
+                reinterpret_cast<const f32x4*>(S.src2 + 128 * k + 2 * lane));
+            nx[k] = make_float4(r[0], r[1], r[2], r[3]);
+        }
+    };
+    auto stage_end = [&](Stage& S) {
+        if (!S.ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
+            Raw tile[NG];
+#pragma unroll
+            for (int k = 0; k < NG; ++k) tile[k] = S.keep[k < NKO ? 0 : k - NKO];
+            roll_hist(hr, tile);
+        }
+        if (!S.fast2 && ld.ok) load_tile(nx, ld);
+    };
+
+    if constexpr (!STAG) {
+        // interleaved: each wave stages tile k+1 (and prefetches tile k+2) group by group
+        // between tile k's MFMA chunks; the two waves of a SIMD overlap as they will
         auto body = [&](auto tau_c) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
-            const bool fast2 = ld.ok && tile_fast(ld);
-            const bool ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
-            // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
-            const long j2 = tile_j0(ld);
-            const float2* src2 = fast2 ? p.in + ld.ch() * p.ld_in + j2 : p.dummy;
-            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch() * (p.ld_in / 2) + (j2 >> 1)
-                                          : reinterpret_cast<const unsigned*>(p.dummy);
-            const int s_next = window_scale(nx, hr);
-            const float scn = exp2i(s_next);
-            constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
-            Raw keep[NK];
+            Stage S;
+            stage_begin(S);
             f32x4 cr[CS], ci[CS];
 #pragma unroll
             for (int j = 0; j < CS; ++j) {
@@ -445,101 +556,26 @@ void fir_mxh_kernel(MxhParams p) {
                 ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             u32x4 fb[2][4];
-            // column set j of the tile reads 256 samples (D = 1) further into the window
-            auto read_frags = [&](u32x4 (&f)[4], int c, int j) {
-                const int a = rb[c] + TAU * WINB + j * 2 * 256 * D;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (!U8 || (q & 1) == 0)
-                        f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
-            };
-            read_frags(fb[0], 0, 0);
-            // D = 1: column set j + 1's chunk 0 reads the window span of set j's last chunk
-            // (256 samples = NCH - 1 chunks of 32 further), so that fragment is not re-read:
-            // the slot of chunk i is (i - j) & 1
-            constexpr bool kShare = D == 1 && 32 * (NCH - 1) == 256;
+            read_frags(fb[0], TAU, 0, 0);
 #pragma unroll
             for (int i = 0; i < CS * NCH; ++i) {
-                const int j = i / NCH, c = i % NCH;
+                const int j = i / NCH;
                 {
                     const int ni = i + 1;
                     const bool reuse = kShare && ni % NCH == 0;
                     if (ni < CS * NCH && !reuse)
-                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], ni % NCH, ni / NCH);
+                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], TAU, ni % NCH, ni / NCH);
                     __builtin_amdgcn_sched_barrier(0);
-                    const u32x4(&f)[4] = fb[(kShare ? i - j : i) & 1];
-                    cr[j] = mfma(al[c], f[0], cr[j]);
-                    ci[j] = mfma(al[c], f[2], ci[j]);
-                    if (!U8) {
-                        cr[j] = mfma(ah[c], f[1], cr[j]);
-                        ci[j] = mfma(ah[c], f[3], ci[j]);
-                    }
-                    cr[j] = mfma(ah[c], f[0], cr[j]);
-                    ci[j] = mfma(ah[c], f[2], ci[j]);
+                    mfma_chunk(cr, ci, fb[(kShare ? i - j : i) & 1], i);
                 }
-                if (i == 0) {  // window k+1's history (old hr); then tile k+2's, if it opens a run
+                if (i == 0) stage_hist(S, WN);
 #pragma unroll
-                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
-                    if (ld_run) load_hist(hr, ld);
-                }
-#pragma unroll
-                for (int k = 0; k < NG; ++k) {
-                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) != i) continue;
-                    put(WN + new_addr(k), nx[k], scn);
-                    if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
-                    if constexpr (U8) {
-                        nx[k] = __builtin_nontemporal_load(src2u + 64 * k + lane);
-                    } else {
-                        const f32x4 r = __builtin_nontemporal_load(
-                            reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane));
-                        nx[k] = make_float4(r[0], r[1], r[2], r[3]);
-                    }
-                }
+                for (int k = 0; k < NG; ++k)
+                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) == i) stage_group(S, WN, k);
             }
-            if (!ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
-                Raw tile[NG];
-#pragma unroll
-                for (int k = 0; k < NG; ++k) tile[k] = keep[k < (NG > NH ? NG - NH : 0) ? 0 : k - (NG > NH ? NG - NH : 0)];
-                roll_hist(hr, tile);
-            }
-            if (!fast2 && ld.ok) load_tile(nx, ld);
-            const int so = -(s_cur + p.sh);
-            float2* __restrict__ out = p.out + cm.ch() * p.ld_out;
-            const long m0 = (long)(cm.tu + cm.t) * G::TO;
-#pragma unroll
-            for (int j = 0; j < CS; ++j) {
-                const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
-                float yr[4], yi[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
-                    yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
-                }
-                if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
-                    // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
-                    // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
-                    // line) and the second those of the odd-v blocks (steady-state probe: 0.472
-                    // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
-                    const bool ev = (v & 1) == 0;
-                    const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                    const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                    f32x4 rx;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
-                            __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
-                    const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
-                    f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
-                    f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
-                    __builtin_nontemporal_store(ev ? y0 : rx, o4);
-                    __builtin_nontemporal_store(ev ? rx : y1, p4);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
-                }
-            }
-            s_cur = s_next;
+            stage_end(S);
+            store_out(cr, ci, cm, s_cur);
+            s_cur = S.s_next;
             cm = st;
             st = ld;
             adv(ld);
@@ -550,6 +586,58 @@ void fir_mxh_kernel(MxhParams p) {
             if (!cm.ok) break;
             body(std::integral_constant<int, 1>());
         }
+    } else {
+        // staggered: every tile is an MFMA phase (tile k's 10 chunks back to back) and a staging
+        // phase (tile k's stores, tile k+1's staging, tile k+2's prefetch), separated by raw
+        // workgroup barriers; waves 4-7 run one phase behind waves 0-3, so on every SIMD one
+        // wave issues MFMAs while the other stages in their shadow.  Waves own their LDS
+        // windows, so the barriers order no data -- they only pace the phases -- and every wave
+        // passes exactly 2T + 1 of them: T = the workgroup's largest tile count (its wave 0's
+        // units x tiles per unit), idle iterations included.
+        static_assert(CS == 1 && !kShare, "staggered phases: D = 4 tiles");
+        const int T = ONE ? (int)(((Idx)p.units - (Idx)blockIdx.x * kWaves + (Idx)nwaves - 1) / (Idx)nwaves) *
+                                (int)p.seg_tiles
+                          : 0;
+        const bool late = wv >= kWaves / 2;
+        if (late) __builtin_amdgcn_s_barrier();
+        auto body_s = [&](auto tau_c) {
+            constexpr int TAU = decltype(tau_c)::value;
+            constexpr int WN = (1 - TAU) * WINB;
+            f32x4 cr[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, ci[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+            if (cm.ok) {
+                u32x4 fb[2][4];
+                read_frags(fb[0], TAU, 0, 0);
+                __builtin_amdgcn_s_setprio(1);  // the MFMA phase wins issue against the stager
+#pragma unroll
+                for (int i = 0; i < NCH; ++i) {
+                    if (i + 1 < NCH) read_frags(fb[(i + 1) & 1], TAU, i + 1, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma_chunk(cr, ci, fb[i & 1], i);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(0);
+            }
+            __builtin_amdgcn_s_barrier();
+            if (cm.ok) {
+                store_out(cr, ci, cm, s_cur);
+                Stage S;
+                stage_begin(S);
+                stage_hist(S, WN);
+#pragma unroll
+                for (int k = 0; k < NG; ++k) stage_group(S, WN, k);
+                stage_end(S);
+                s_cur = S.s_next;
+            }
+            __builtin_amdgcn_s_barrier();
+            cm = st;
+            st = ld;
+            adv(ld);
+        };
+        for (int it = 0; it < T; it += 2) {
+            body_s(std::integral_constant<int, 0>());
+            if (it + 1 < T) body_s(std::integral_constant<int, 1>());
+        }
+        if (!late) __builtin_amdgcn_s_barrier();
     }
 
     if (p.hist_next) {  // stream history carry, spread over the whole grid
@@ -650,7 +738,7 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     const bool one = !u8 && D == 4 && nch == 1 && !p.blocked && p.units < (1L << 30) &&
                      p.tpc < (1L << 30);
 #define SDRGPU_MXH_GO(CC, U, DD, CS, ONE)                                                      \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE>), dim3(blocks), dim3(kBlock),       \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE, ONE>), dim3(blocks), dim3(kBlock),  \
                        (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
