@@ -241,15 +241,8 @@ s = s.replace(old, """                    const int ni = i + (D == 4 ? 2 : 1);
                     const u32x4(&f)[4] = fb[D == 4 ? i % 3 : (kShare ? i - j : i) & 1];""")
 open(p, 'w').write(s)
 PY
-  elif [ $part = nostag ]; then  # the ONE launch without staggered phases (interleaved body)
-    python3 - $src <<'PY'
-import sys
-p = sys.argv[1]; s = open(p).read()
-old = "fir_mxh_kernel<CC, U, DD, CS, ONE, ONE>"
-assert old in s
-s = s.replace(old, "fir_mxh_kernel<CC, U, DD, CS, ONE, false>")
-open(p, 'w').write(s)
-PY
+  elif [ $part = stag ]; then  # staggered MFMA / staging phases for the ONE launch (tools/experiments/fir_mxh_staggered.patch; round 4: slower, not kept)
+    patch -s $src tools/experiments/fir_mxh_staggered.patch
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys

@@ -218,7 +218,7 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // samples apart already hit distinct banks; identity block map).
 // ONE: a single channel dealt grid-strided (the headline shape): cursors are 32-bit unit /
 // tile indices with no channel arithmetic (no 64-bit division per unit, no SGPR spills).
-template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false, bool STAG = false>
+template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
@@ -233,7 +233,7 @@ void fir_mxh_kernel(MxhParams p) {
     // the younger half of the workgroup (waves 4-7) loses VALU arbitration to its SIMD partner
     // on every segment (priority, then age): one static s_setprio 1 for it, no per-segment
     // flips (configs[1]: 0.5229 -> 0.5189 ms over 3 A/B reps, profiles/r02_fir_prio_ab.txt)
-    if (!STAG && wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
+    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
     const long wave = (long)blockIdx.x * kWaves + wv;
     const long nwaves = (long)gridDim.x * kWaves;
     const int g = lane >> 4, v = lane & 15;
@@ -402,12 +402,11 @@ void fir_mxh_kernel(MxhParams p) {
 
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
-    static_assert(!STAG || ONE, "staggered phases: single-channel dealing");
     Cur cm{}, st{}, ld{};
     seek(cm, ONE ? (Idx)wave : (p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave));
     Raw nx[NG], hr[NH];
     int s_cur = 0;
-    if (!STAG && cm.ok) {
+    if (cm.ok) {
         load_hist(hr, cm);
         load_tile(nx, cm);
         s_cur = window_scale(nx, hr);
@@ -541,7 +540,7 @@ void fir_mxh_kernel(MxhParams p) {
         if (!S.fast2 && ld.ok) load_tile(nx, ld);
     };
 
-    if constexpr (!STAG) {
+    {
         // interleaved: each wave stages tile k+1 (and prefetches tile k+2) group by group
         // between tile k's MFMA chunks; the two waves of a SIMD overlap as they will
         auto body = [&](auto tau_c) {
@@ -586,103 +585,6 @@ void fir_mxh_kernel(MxhParams p) {
             if (!cm.ok) break;
             body(std::integral_constant<int, 1>());
         }
-    } else {
-        // staggered: every tile is an MFMA phase (tile k's 10 chunks back to back) and a staging
-        // phase (tile k's stores, tile k+1's staging, tile k+3's loads), separated by raw
-        // workgroup barriers; waves 4-7 run one phase behind waves 0-3, so on every SIMD one
-        // wave issues MFMAs while the other stages in their shadow.  Two raw tiles per wave are
-        // in flight (register sets 0 / 1, alternating with the LDS window halves), so a tile's
-        // loads have two whole iterations to land.  Waves own their LDS windows, so the barriers
-        // order no data -- they only pace the phases -- and every wave passes exactly 2T + 1 of
-        // them: T = the workgroup's largest tile count (its wave 0's units x tiles per unit),
-        // idle iterations included.
-        static_assert(CS == 1 && !kShare && NH <= NG, "staggered phases: D = 4 tiles");
-        const int T = ONE ? (int)(((Idx)p.units - (Idx)blockIdx.x * kWaves + (Idx)nwaves - 1) / (Idx)nwaves) *
-                                (int)p.seg_tiles
-                          : 0;
-        Raw rx[2][NG], rh[2][NH], keep[NH];  // raw tiles (+ unit-start history) in flight; tail of the last staged tile
-        Cur l2{};
-        // raw data of tile c into set q: its groups, and its history when it opens a unit
-        auto issue = [&](int q, const Cur& c) {
-            if (!c.ok) return;
-            if (c.t == 0) load_hist(rh[q], c);
-            load_tile(rx[q], c);
-        };
-        if (cm.ok) {
-            issue(1, cm);
-            s_cur = window_scale(rx[1], rh[1]);
-            const float sc = exp2i(s_cur);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) put(hist_addr(k), rh[1][k], sc);
-#pragma unroll
-            for (int k = 0; k < NG; ++k) put(new_addr(k), rx[1][k], sc);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) keep[k] = rx[1][NG - NH + k];
-            st = cm;
-            adv(st);
-            issue(0, st);
-            ld = st;
-            adv(ld);
-            issue(1, ld);
-            l2 = ld;
-            adv(l2);
-        }
-        const bool late = wv >= kWaves / 2;
-        if (late) __builtin_amdgcn_s_barrier();
-        auto body_s = [&](auto tau_c) {
-            constexpr int TAU = decltype(tau_c)::value;  // LDS half of tile cm, register set of tile st
-            constexpr int WN = (1 - TAU) * WINB;
-            f32x4 cr[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, ci[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
-            if (cm.ok) {
-                u32x4 fb[2][4];
-                read_frags(fb[0], TAU, 0, 0);
-                __builtin_amdgcn_s_setprio(1);  // the MFMA phase wins issue against the stager
-#pragma unroll
-                for (int i = 0; i < NCH; ++i) {
-                    if (i + 1 < NCH) read_frags(fb[(i + 1) & 1], TAU, i + 1, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma_chunk(cr, ci, fb[i & 1], i);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_setprio(0);
-            }
-            __builtin_amdgcn_s_barrier();
-            if (cm.ok) store_out(cr, ci, cm, s_cur);
-            if (st.ok) {
-                Raw (&x)[NG] = rx[TAU];
-                Raw h[NH];
-#pragma unroll
-                for (int k = 0; k < NH; ++k) h[k] = st.t == 0 ? rh[TAU][k] : keep[k];
-                const int sn = window_scale(x, h);
-                const float scn = exp2i(sn);
-#pragma unroll
-                for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), h[k], scn);
-                // tile l2's loads reuse the set as its groups are staged
-                const bool fast = l2.ok && tile_fast(l2);
-                const float2* src = fast ? p.in + tile_j0(l2) : p.dummy;
-                if (l2.ok && l2.t == 0) load_hist(rh[TAU], l2);
-#pragma unroll
-                for (int k = 0; k < NG; ++k) {
-                    put(WN + new_addr(k), x[k], scn);
-                    if (k >= NG - NH) keep[k - (NG - NH)] = x[k];
-                    const f32x4 r = __builtin_nontemporal_load(
-                        reinterpret_cast<const f32x4*>(src + 128 * k + 2 * lane));
-                    x[k] = make_float4(r[0], r[1], r[2], r[3]);
-                }
-                if (!fast && l2.ok) load_tile(x, l2);
-                s_cur = sn;
-            }
-            __builtin_amdgcn_s_barrier();
-            cm = st;
-            st = ld;
-            ld = l2;
-            adv(l2);
-        };
-        for (int it = 0; it < T; it += 2) {
-            body_s(std::integral_constant<int, 0>());
-            if (it + 1 < T) body_s(std::integral_constant<int, 1>());
-        }
-        if (!late) __builtin_amdgcn_s_barrier();
     }
 
     if (p.hist_next) {  // stream history carry, spread over the whole grid
@@ -783,7 +685,7 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     const bool one = !u8 && D == 4 && nch == 1 && !p.blocked && p.units < (1L << 30) &&
                      p.tpc < (1L << 30);
 #define SDRGPU_MXH_GO(CC, U, DD, CS, ONE)                                                      \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE, ONE>), dim3(blocks), dim3(kBlock),  \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE>), dim3(blocks), dim3(kBlock),       \
                        (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
