@@ -17,6 +17,7 @@ from sdrgpu.device import DeviceBuffer  # noqa: E402
 from test_pll_gpu import RATE, fm_channels, main_rs_design, oracle_params  # noqa: E402
 
 nch, n, cut = 1024, 9000, int(sys.argv[1]) if len(sys.argv) > 1 else 3002
+mode = sys.argv[2] if len(sys.argv) > 2 else "chain"  # chain | serial (PLL synced before the next bank block) | pllonly
 rng = np.random.default_rng(45 + nch)
 x = fm_channels(rng, nch, n)
 taps = ss.firwin(255, 0.2).astype(np.float32)
@@ -26,17 +27,35 @@ dx = DeviceBuffer.from_numpy(x)
 dy = DeviceBuffer.empty(nch * n, np.complex64)
 do = DeviceBuffer.empty(nch * n, np.float32)
 dl = DeviceBuffer.empty(nch * n, np.uint8)
-for a, e in ((0, cut), (cut, n)):
-    assert b.process_dev(dx.ptr + 8 * a, n, e - a, dy.ptr + 8 * a, n) == e - a
+if mode == "pllonly":  # bank over the whole rows first, then the PLL in the two blocks
+    assert b.process_dev(dx.ptr, n, n, dy.ptr, n) == n
     b.sync()
+from sdrgpu.device import synchronize  # noqa: E402
+dz = DeviceBuffer.empty(nch * n, np.complex64) if mode == "otherbuf" else None
+for a, e in ((0, cut), (cut, n)):
+    if mode != "pllonly":
+        tgt = dz if (mode == "otherbuf" and a > 0) else dy
+        assert b.process_dev(dx.ptr + 8 * a, n, e - a, tgt.ptr + 8 * a, n) == e - a
+        b.sync()
+        if mode == "devsync":
+            synchronize(0)
+        if mode == "otherbuf" and a > 0:  # block 2 went to dz: copy its columns into dy afterwards
+            pass
     pll.process_dev(dy.ptr + 8 * a, n, e - a, do.ptr + 4 * a, dl.ptr + a, n)
+    if mode in ("serial", "pllonly"):
+        pll.sync()
 pll.sync()
+if mode == "otherbuf":  # dy's block-2 columns from dz (row by row) so the oracle sees what the PLL read
+    yz = dz.download().reshape(nch, n)
+    yy = dy.download().reshape(nch, n)
+    yy[:, cut:] = yz[:, cut:]
+    dy.upload(np.ascontiguousarray(yy.reshape(-1)))
 y = dy.download().reshape(nch, n)
 out = do.download(dtype=np.float32).reshape(nch, n)
 lk = dl.download(dtype=np.uint8).reshape(nch, n)
 ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), y, nthreads=16)
 bad = np.nonzero(((out != ref_out) & ~(np.isnan(out) & np.isnan(ref_out))) | (lk != ref_lk))
-print("cut", cut, "mismatching samples", bad[0].size, "channels", np.unique(bad[0])[:20])
+print("mode", mode, "cut", cut, "mismatching samples", bad[0].size, "channels", np.unique(bad[0])[:20])
 if bad[0].size:
     c = int(bad[0][0])
     first = int(bad[1][bad[0] == c].min())
