@@ -243,6 +243,17 @@ open(p, 'w').write(s)
 PY
   elif [ $part = stag ]; then  # staggered MFMA / staging phases for the ONE launch (tools/experiments/fir_mxh_staggered.patch; round 4: slower, not kept)
     patch -s $src tools/experiments/fir_mxh_staggered.patch
+  elif [ $part = noone ]; then  # the ONE instantiation compiled but never launched (bisect)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    const bool one = !u8 && D == 4"
+assert old in s
+s = s.replace(old, "    const bool one = false && !u8 && D == 4")
+open(p, 'w').write(s)
+PY
+  elif [ $part = r3src ]; then  # the round-3 fir_mxh.hip (commit 76500ef), rebuilt (bisect)
+    cp tools/experiments/fir_mxh_r3.hip $src
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys
