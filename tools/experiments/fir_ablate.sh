@@ -254,6 +254,8 @@ open(p, 'w').write(s)
 PY
   elif [ $part = r3src ]; then  # the round-3 fir_mxh.hip (commit 76500ef), rebuilt (bisect)
     cp tools/experiments/fir_mxh_r3.hip $src
+  elif [ $part = one ]; then  # round 4's ONE instantiation + factored body (tools/experiments/fir_mxh_one.hip): faster, but the configs[3] chain test mismatches beside it
+    cp tools/experiments/fir_mxh_one.hip $src
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys

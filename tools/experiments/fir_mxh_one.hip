@@ -216,7 +216,9 @@ __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1
 // 2 MFMAs per component per chunk.
 // D: decimation 4 (XOR-swizzled LDS rows, block map sigma) or 1 (linear LDS: blocks 16
 // samples apart already hit distinct banks; identity block map).
-template <int NCH, bool U8 = false, int D = 4, int CS = 1>
+// ONE: a single channel dealt grid-strided (the headline shape): cursors are 32-bit unit /
+// tile indices with no channel arithmetic (no 64-bit division per unit, no SGPR spills).
+template <int NCH, bool U8 = false, int D = 4, int CS = 1, bool ONE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
@@ -288,19 +290,28 @@ void fir_mxh_kernel(MxhParams p) {
     // computed and stored, k+1 staged, k+2 loading) advance together, so the raw-tile
     // prefetch crosses run boundaries; a run's first window re-reads the H samples before it
     // (issued one tile ahead, into the history registers).
+    using Idx = std::conditional_t<ONE, int, long>;
     struct Cur {
-        long u, t, ch, tu, nt;
+        Idx u, t, tu, nt;
+        long ch_;
         bool ok;
+        __device__ long ch() const { return ONE ? 0L : ch_; }
     };
-    const long ust = p.blocked ? (long)kWaves : nwaves;
-    const long ub1 = p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units;
-    auto seek = [&](Cur& c, long u) {
+    const Idx ust = ONE ? (Idx)nwaves : (p.blocked ? (long)kWaves : nwaves);
+    const Idx ub1 = ONE ? (Idx)p.units : (p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units);
+    auto seek = [&](Cur& c, Idx u) {
         c.u = u;
         c.t = 0;
         c.ok = u < ub1;
-        c.ch = c.ok ? u / p.spc : 0;
-        c.tu = (u - c.ch * p.spc) * p.seg_tiles;
-        c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        if constexpr (ONE) {
+            c.ch_ = 0;
+            c.tu = u * (Idx)p.seg_tiles;
+            c.nt = c.ok ? std::min((Idx)p.seg_tiles, (Idx)p.tpc - c.tu) : 0;
+        } else {
+            c.ch_ = c.ok ? u / p.spc : 0;
+            c.tu = (u - c.ch_ * p.spc) * p.seg_tiles;
+            c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        }
         if (c.ok && c.nt <= 0) c.ok = false;  // (units past a channel's last tile: none by construction)
     };
     auto adv = [&](Cur& c) {
@@ -311,12 +322,12 @@ void fir_mxh_kernel(MxhParams p) {
     auto tile_j0 = [&](const Cur& c) { return (long)TI * (c.tu + c.t); };
     auto tile_fast = [&](const Cur& c) { return (long)TI * (c.tu + c.t + 1) <= n_in; };
     auto fetch = [&](const Cur& c, long j) -> Raw {
-        const float2* hist = p.hist + c.ch * (long)(K - 1);
+        const float2* hist = p.hist + c.ch() * (long)(K - 1);
         if constexpr (U8)
-            return fetch_pair_u8(reinterpret_cast<const unsigned short*>(p.in_u8) + c.ch * p.ld_in, hist, j,
+            return fetch_pair_u8(reinterpret_cast<const unsigned short*>(p.in_u8) + c.ch() * p.ld_in, hist, j,
                                  n_in, K);
         else
-            return fetch_pair(p.in + c.ch * p.ld_in, hist, j, n_in, K);
+            return fetch_pair(p.in + c.ch() * p.ld_in, hist, j, n_in, K);
     };
     auto put = [&](int a, const Raw& w, float sc) {
         if constexpr (U8) put_pair_u8<PLB>(smem, a, w);
@@ -326,10 +337,10 @@ void fir_mxh_kernel(MxhParams p) {
     auto ldx = [&](const Cur& c, long j, auto nt_c) -> Raw {
         constexpr bool NT = decltype(nt_c)::value;
         if constexpr (U8) {
-            const unsigned* q = p.in_u8 + c.ch * (p.ld_in / 2) + (j >> 1);
+            const unsigned* q = p.in_u8 + c.ch() * (p.ld_in / 2) + (j >> 1);
             return NT ? __builtin_nontemporal_load(q) : *q;
         } else {
-            const f32x4* q = reinterpret_cast<const f32x4*>(p.in + c.ch * p.ld_in + j);
+            const f32x4* q = reinterpret_cast<const f32x4*>(p.in + c.ch() * p.ld_in + j);
             const f32x4 r = NT ? __builtin_nontemporal_load(q) : *q;
             return make_float4(r[0], r[1], r[2], r[3]);
         }
@@ -391,13 +402,14 @@ void fir_mxh_kernel(MxhParams p) {
 
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
-    Cur cm, st, ld;
-    seek(cm, p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave);
+    Cur cm{}, st{}, ld{};
+    seek(cm, ONE ? (Idx)wave : (p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave));
+    Raw nx[NG], hr[NH];
+    int s_cur = 0;
     if (cm.ok) {
-        Raw nx[NG], hr[NH];
         load_hist(hr, cm);
         load_tile(nx, cm);
-        int s_cur = window_scale(nx, hr);
+        s_cur = window_scale(nx, hr);
         {
             const float sc = exp2i(s_cur);
 #pragma unroll
@@ -412,21 +424,130 @@ void fir_mxh_kernel(MxhParams p) {
         if (st.ok) load_tile(nx, st);
         ld = st;
         adv(ld);
+    }
 
+    constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
+    constexpr int NKO = NG > NH ? NG - NH : 0;
+    // column set j of the tile reads 256 samples (D = 1) further into the window
+    auto read_frags = [&](u32x4 (&f)[4], int tau, int c, int j) {
+        const int a = rb[c] + tau * WINB + j * 2 * 256 * D;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (!U8 || (q & 1) == 0)
+                f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
+    };
+    // D = 1: column set j + 1's chunk 0 reads the window span of set j's last chunk
+    // (256 samples = NCH - 1 chunks of 32 further), so that fragment is not re-read:
+    // the slot of chunk i is (i - j) & 1
+    constexpr bool kShare = D == 1 && 32 * (NCH - 1) == 256;
+    // chunk i's MFMAs on fragment slot f
+    auto mfma_chunk = [&](f32x4 (&cr)[CS], f32x4 (&ci)[CS], const u32x4 (&f)[4], int i) {
+        const int j = i / NCH, c = i % NCH;
+        cr[j] = mfma(al[c], f[0], cr[j]);
+        ci[j] = mfma(al[c], f[2], ci[j]);
+        if (!U8) {
+            cr[j] = mfma(ah[c], f[1], cr[j]);
+            ci[j] = mfma(ah[c], f[3], ci[j]);
+        }
+        cr[j] = mfma(ah[c], f[0], cr[j]);
+        ci[j] = mfma(ah[c], f[2], ci[j]);
+    };
+    // tile c's outputs (accumulators scaled back by 2^-(s + sh)) to HBM
+    auto store_out = [&](const f32x4 (&cr)[CS], const f32x4 (&ci)[CS], const Cur& c, int s) {
+        const int so = -(s + p.sh);
+        float2* __restrict__ out = p.out + c.ch() * p.ld_out;
+        const long m0 = (long)(c.tu + c.t) * G::TO;
+#pragma unroll
+        for (int j = 0; j < CS; ++j) {
+            const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
+            float yr[4], yi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
+                yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
+            }
+            if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
+                // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
+                // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
+                // line) and the second those of the odd-v blocks (steady-state probe: 0.472
+                // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
+                const bool ev = (v & 1) == 0;
+                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                f32x4 rx;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
+                        __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
+                const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
+                f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
+                f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
+                __builtin_nontemporal_store(ev ? y0 : rx, o4);
+                __builtin_nontemporal_store(ev ? rx : y1, p4);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+            }
+        }
+    };
+    // staging of tile st into the window buffer at byte offset wn (its history groups first,
+    // then each new group k, whose registers then take group k of tile ld: the prefetch);
+    // stage_group(k) runs after chunk k's MFMAs in the interleaved body, all at once in the
+    // staggered one
+    struct Stage {
+        bool fast2, ld_run;
+        const float2* src2;
+        const unsigned* src2u;
+        int s_next;
+        float scn;
+        Raw keep[NK];
+    };
+    auto stage_begin = [&](Stage& S) {
+        S.fast2 = ld.ok && tile_fast(ld);
+        S.ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
+        // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
+        const long j2 = tile_j0(ld);
+        S.src2 = S.fast2 ? p.in + ld.ch() * p.ld_in + j2 : p.dummy;
+        S.src2u = S.fast2 ? p.in_u8 + ld.ch() * (p.ld_in / 2) + (j2 >> 1)
+                          : reinterpret_cast<const unsigned*>(p.dummy);
+        S.s_next = window_scale(nx, hr);
+        S.scn = exp2i(S.s_next);
+    };
+    auto stage_hist = [&](Stage& S, int wn) {  // window k+1's history (old hr); then tile k+2's
+#pragma unroll
+        for (int k = 0; k < NH; ++k) put(wn + hist_addr(k), hr[k], S.scn);
+        if (S.ld_run) load_hist(hr, ld);
+    };
+    auto stage_group = [&](Stage& S, int wn, int k) {
+        put(wn + new_addr(k), nx[k], S.scn);
+        if (k >= NG - NH) S.keep[k - NKO] = nx[k];
+        if constexpr (U8) {
+            nx[k] = __builtin_nontemporal_load(S.src2u + 64 * k + lane);
+        } else {
+            const f32x4 r = __builtin_nontemporal_load(
+                reinterpret_cast<const f32x4*>(S.src2 + 128 * k + 2 * lane));
+            nx[k] = make_float4(r[0], r[1], r[2], r[3]);
+        }
+    };
+    auto stage_end = [&](Stage& S) {
+        if (!S.ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
+            Raw tile[NG];
+#pragma unroll
+            for (int k = 0; k < NG; ++k) tile[k] = S.keep[k < NKO ? 0 : k - NKO];
+            roll_hist(hr, tile);
+        }
+        if (!S.fast2 && ld.ok) load_tile(nx, ld);
+    };
+
+    {
+        // interleaved: each wave stages tile k+1 (and prefetches tile k+2) group by group
+        // between tile k's MFMA chunks; the two waves of a SIMD overlap as they will
         auto body = [&](auto tau_c) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
-            const bool fast2 = ld.ok && tile_fast(ld);
-            const bool ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
-            // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
-            const long j2 = tile_j0(ld);
-            const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;
-            const unsigned* src2u = fast2 ? p.in_u8 + ld.ch * (p.ld_in / 2) + (j2 >> 1)
-                                          : reinterpret_cast<const unsigned*>(p.dummy);
-            const int s_next = window_scale(nx, hr);
-            const float scn = exp2i(s_next);
-            constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
-            Raw keep[NK];
+            Stage S;
+            stage_begin(S);
             f32x4 cr[CS], ci[CS];
 #pragma unroll
             for (int j = 0; j < CS; ++j) {
@@ -434,101 +555,26 @@ void fir_mxh_kernel(MxhParams p) {
                 ci[j] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             u32x4 fb[2][4];
-            // column set j of the tile reads 256 samples (D = 1) further into the window
-            auto read_frags = [&](u32x4 (&f)[4], int c, int j) {
-                const int a = rb[c] + TAU * WINB + j * 2 * 256 * D;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (!U8 || (q & 1) == 0)
-                        f[q] = *reinterpret_cast<const u32x4*>(smem + a + q * PLB);
-            };
-            read_frags(fb[0], 0, 0);
-            // D = 1: column set j + 1's chunk 0 reads the window span of set j's last chunk
-            // (256 samples = NCH - 1 chunks of 32 further), so that fragment is not re-read:
-            // the slot of chunk i is (i - j) & 1
-            constexpr bool kShare = D == 1 && 32 * (NCH - 1) == 256;
+            read_frags(fb[0], TAU, 0, 0);
 #pragma unroll
             for (int i = 0; i < CS * NCH; ++i) {
-                const int j = i / NCH, c = i % NCH;
+                const int j = i / NCH;
                 {
                     const int ni = i + 1;
                     const bool reuse = kShare && ni % NCH == 0;
                     if (ni < CS * NCH && !reuse)
-                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], ni % NCH, ni / NCH);
+                        read_frags(fb[(kShare ? ni - ni / NCH : ni) & 1], TAU, ni % NCH, ni / NCH);
                     __builtin_amdgcn_sched_barrier(0);
-                    const u32x4(&f)[4] = fb[(kShare ? i - j : i) & 1];
-                    cr[j] = mfma(al[c], f[0], cr[j]);
-                    ci[j] = mfma(al[c], f[2], ci[j]);
-                    if (!U8) {
-                        cr[j] = mfma(ah[c], f[1], cr[j]);
-                        ci[j] = mfma(ah[c], f[3], ci[j]);
-                    }
-                    cr[j] = mfma(ah[c], f[0], cr[j]);
-                    ci[j] = mfma(ah[c], f[2], ci[j]);
+                    mfma_chunk(cr, ci, fb[(kShare ? i - j : i) & 1], i);
                 }
-                if (i == 0) {  // window k+1's history (old hr); then tile k+2's, if it opens a run
+                if (i == 0) stage_hist(S, WN);
 #pragma unroll
-                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
-                    if (ld_run) load_hist(hr, ld);
-                }
-#pragma unroll
-                for (int k = 0; k < NG; ++k) {
-                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) != i) continue;
-                    put(WN + new_addr(k), nx[k], scn);
-                    if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
-                    if constexpr (U8) {
-                        nx[k] = __builtin_nontemporal_load(src2u + 64 * k + lane);
-                    } else {
-                        const f32x4 r = __builtin_nontemporal_load(
-                            reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane));
-                        nx[k] = make_float4(r[0], r[1], r[2], r[3]);
-                    }
-                }
+                for (int k = 0; k < NG; ++k)
+                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) == i) stage_group(S, WN, k);
             }
-            if (!ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
-                Raw tile[NG];
-#pragma unroll
-                for (int k = 0; k < NG; ++k) tile[k] = keep[k < (NG > NH ? NG - NH : 0) ? 0 : k - (NG > NH ? NG - NH : 0)];
-                roll_hist(hr, tile);
-            }
-            if (!fast2 && ld.ok) load_tile(nx, ld);
-            const int so = -(s_cur + p.sh);
-            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            const long m0 = (cm.tu + cm.t) * G::TO;
-#pragma unroll
-            for (int j = 0; j < CS; ++j) {
-                const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
-                float yr[4], yi[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
-                    yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
-                }
-                if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
-                    // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
-                    // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
-                    // line) and the second those of the odd-v blocks (steady-state probe: 0.472
-                    // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
-                    const bool ev = (v & 1) == 0;
-                    const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                    const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                    f32x4 rx;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
-                            __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
-                    const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
-                    f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
-                    f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
-                    __builtin_nontemporal_store(ev ? y0 : rx, o4);
-                    __builtin_nontemporal_store(ev ? rx : y1, p4);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
-                }
-            }
-            s_cur = s_next;
+            stage_end(S);
+            store_out(cr, ci, cm, s_cur);
+            s_cur = S.s_next;
             cm = st;
             st = ld;
             adv(ld);
@@ -635,19 +681,23 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     p.units = nch * p.spc;
     p.blocked = run > 0 && u8;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
-#define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
-    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
+    // one channel dealt grid-strided with 32-bit unit indices: the ONE instantiation
+    const bool one = !u8 && D == 4 && nch == 1 && !p.blocked && p.units < (1L << 30) &&
+                     p.tpc < (1L << 30);
+#define SDRGPU_MXH_GO(CC, U, DD, CS, ONE)                                                      \
+    hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS, ONE>), dim3(blocks), dim3(kBlock),       \
                        (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)
 #define SDRGPU_MXH_CASE(CC)                                                                    \
     if (D == 4 && NCH == CC) {                                                                 \
-        if (u8) SDRGPU_MXH_GO(CC, true, 4, 1);                                                 \
-        else SDRGPU_MXH_GO(CC, false, 4, 1);                                                   \
+        if (u8) SDRGPU_MXH_GO(CC, true, 4, 1, false);                                          \
+        else if (one) SDRGPU_MXH_GO(CC, false, 4, 1, true);                                    \
+        else SDRGPU_MXH_GO(CC, false, 4, 1, false);                                            \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
 #define SDRGPU_MXH_CASE1(CC)                                                                   \
     if (D == 1 && NCH == CC) {                                                                 \
-        SDRGPU_MXH_GO(CC, false, 1, kCs1);                                                     \
+        SDRGPU_MXH_GO(CC, false, 1, kCs1, false);                                              \
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
