@@ -18,6 +18,7 @@ from test_pll_gpu import RATE, fm_channels, main_rs_design, oracle_params  # noq
 nch, n = 1024, 9000
 cut = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
 pad = int(sys.argv[2]) if len(sys.argv) > 2 else 0   # extra MiB allocated before dy (address shift)
+scalar = len(sys.argv) > 3 and sys.argv[3] == "scalar"  # lock flags at an odd address: the PLL's LDS-free pll_kernel<..., false>
 rng = np.random.default_rng(45 + nch)
 x = fm_channels(rng, nch, n)
 taps = ss.firwin(255, 0.2).astype(np.float32)
@@ -28,24 +29,25 @@ spacer = DeviceBuffer(pad << 20) if pad else None
 dy = DeviceBuffer.empty(nch * n, np.complex64)
 dy.fill_zero()
 do = DeviceBuffer.empty(nch * n, np.float32)
-dl = DeviceBuffer.empty(nch * n, np.uint8)
+dl = DeviceBuffer.empty(nch * n + 8, np.uint8)
+lko = 1 if scalar else 0
 assert b.process_dev(dx.ptr, n, cut, dy.ptr, n) == cut
 b.sync()
 y1 = dy.download().reshape(nch, n)
-pll.process_dev(dy.ptr, n, cut, do.ptr, dl.ptr, n)
+pll.process_dev(dy.ptr, n, cut, do.ptr, dl.ptr + lko, n)
 assert b.process_dev(dx.ptr + 8 * cut, n, n - cut, dy.ptr + 8 * cut, n) == n - cut
 b.sync()
 pll.sync()
 y2 = dy.download().reshape(nch, n)
 ch = (y1[:, :cut] != y2[:, :cut])
 rows, cols = np.nonzero(ch)
-print("pad", pad, "MiB  dy[:, :cut] changed during the chain:", int(ch.sum()), "rows", np.unique(rows)[:24],
+print("scalar PLL" if scalar else "split PLL", "pad", pad, "MiB  dy[:, :cut] changed during the chain:", int(ch.sum()), "rows", np.unique(rows)[:24],
       "cols", np.unique(cols)[:16])
 if rows.size:
     r, c = rows[0], cols[0]
     print(" e.g. row", r, "col", c, "after block 1", y1[r, c], "after the chain", y2[r, c])
 out = do.download(dtype=np.float32).reshape(nch, n)[:, :cut]
-lk = dl.download(dtype=np.uint8).reshape(nch, n)[:, :cut]
+lk = dl.download(dtype=np.uint8)[lko:lko + nch * n].reshape(nch, n)[:, :cut]
 for name, yy in (("snapshot after block 1", y1), ("final dy", y2)):
     ro, rl = oracle.pll_batch(oracle_params(oracle), np.ascontiguousarray(yy[:, :cut]), nthreads=16)
     bad = (out != ro) | (lk != rl)
