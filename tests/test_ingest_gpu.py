@@ -95,3 +95,50 @@ def test_cu8_device_path_and_bank(sdr, oracle):
     for c in range(nch):
         ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(x[c]))
         assert_parity(y[c], ref, what=f"bank ch {c}")
+
+
+def test_cu8_int8_and_fp16_kernels(sdr, oracle):
+    """D = 4 u8 blocks take the int8-MFMA kernel (fir_mxi.hip) when the channel bases are
+    16-byte aligned and the fp16 kernel (fir_mxh.hip) when they are only 4-byte aligned; both
+    meet the tolerance on the same stream, including a bank whose leading dimension breaks the
+    16-byte alignment of every other channel (the whole bank then takes the fp16 kernel)."""
+    from sdrgpu import _lib
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(31)
+    for K in (255, 97):  # 5 and 3 K = 64 chunks
+        taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+        n = 3 * 4096 + 1000
+        raw = u8_stream(rng, n)
+        ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
+        for off in (0, 4):  # byte offset of the block: 16-byte aligned, 4-byte aligned
+            f = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+            dx = DeviceBuffer(2 * n + 16)
+            dx.upload(raw, offset_bytes=off)
+            n_out = f.output_len(n)
+            dy = DeviceBuffer.empty(n_out, np.complex64)
+            assert f.process_dev(dx.ptr + off, n, dy.ptr, n_out) == n_out
+            f.sync()
+            assert f.last_algorithm() == _lib.FIR_MATRIX
+            assert_parity(dy.download(), ref, what=f"K{K} offset {off}")
+    taps = (rng.standard_normal(255) / 16).astype(np.float32)
+    for nb in (8192 + 24, 8192 + 26):  # leading dim % 8 == 0 (int8) / != 0 (fp16)
+        nch = 4
+        x = rng.integers(0, 256, size=(nch, 2 * nb), dtype=np.uint8)
+        y = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=4).process(x)
+        for c in range(nch):
+            ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(x[c]))
+            assert_parity(y[c], ref, what=f"bank nb {nb} ch {c}")
+
+
+@pytest.mark.parametrize("scale", [1e-25, 3e-8, 1.0, 5e6, 1e25])
+def test_cu8_tap_scale_range(sdr, oracle, scale):
+    """The int8 kernel takes the taps as 23-bit integers of h 2^(S): any overall tap scale
+    keeps the tolerance (S follows max |h|)."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(77)
+    taps = (rng.standard_normal(255) / 16 * scale).astype(np.float32)
+    raw = u8_stream(rng, 20000)
+    f = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+    y = f.process(raw)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
+    assert_parity(y, ref, what=f"tap scale {scale}")

@@ -52,3 +52,14 @@ for name, yy in (("snapshot after block 1", y1), ("final dy", y2)):
     ro, rl = oracle.pll_batch(oracle_params(oracle), np.ascontiguousarray(yy[:, :cut]), nthreads=16)
     bad = (out != ro) | (lk != rl)
     print(" GPU PLL block 1 vs oracle on the", name + ":", int(bad.sum()), "samples in", np.unique(np.nonzero(bad)[0]).size, "channels")
+    if bad.any() and name == "final dy":
+        chs = np.unique(np.nonzero(bad)[0])
+        first = np.array([np.argmax(bad[c]) for c in chs])
+        fo = np.array([np.argmax(out[c] != ro[c]) if (out[c] != ro[c]).any() else -1 for c in chs])
+        fl = np.array([np.argmax(lk[c] != rl[c]) if (lk[c] != rl[c]).any() else -1 for c in chs])
+        print("  bad channels:", chs.tolist())
+        print("  first bad sample per channel (min/median/max):", int(first.min()), int(np.median(first)), int(first.max()),
+              " histogram by 8-sample chunk:", np.bincount(first // 8).nonzero()[0][:20].tolist())
+        print("  first out mismatch:", fo[:16].tolist(), " first lock mismatch:", fl[:16].tolist())
+        c0 = chs[0]; i0 = first[0]
+        print("  e.g. ch", int(c0), "samples", int(i0), "..", int(i0) + 4, "gpu", out[c0, i0:i0 + 4].tolist(), "oracle", ro[c0, i0:i0 + 4].tolist())

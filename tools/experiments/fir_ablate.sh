@@ -256,6 +256,40 @@ PY
     cp tools/experiments/fir_mxh_r3.hip $src
   elif [ $part = one ]; then  # round 4's ONE instantiation + factored body (tools/experiments/fir_mxh_one.hip): faster, but the configs[3] chain test mismatches beside it
     cp tools/experiments/fir_mxh_one.hip $src
+  elif [ $part = canary ]; then  # D = 1 launches get 16 KiB more LDS (a CU then holds no other workgroup beside a bank workgroup), filled with a pattern and checked at the end (printf CANARY on a change)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = "    extern __shared__ __attribute__((aligned(16))) char smem[];"
+assert old in s
+s = s.replace(old, old + """
+    unsigned* canary = reinterpret_cast<unsigned*>(smem + kWaves * G::WAVE);
+    if constexpr (D == 1) {
+        for (int q = threadIdx.x; q < 4096; q += kBlock) canary[q] = 0xA5A5A5A5u ^ (unsigned)q;
+        __syncthreads();
+    }""")
+old = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
+assert old in s
+s = s.replace(old, """    if constexpr (D == 1) {
+        __syncthreads();
+        int bad = -1;
+        unsigned val = 0;
+        for (int q = threadIdx.x; q < 4096; q += kBlock)
+            if (canary[q] != (0xA5A5A5A5u ^ (unsigned)q) && bad < 0) {
+                bad = q;
+                val = canary[q];
+            }
+        const unsigned long long m = __ballot(bad >= 0);
+        if (m && (threadIdx.x & 63) == __ffsll((long long)m) - 1)
+            printf("CANARY blk %d thr %d dword %d val %08x lanes %016llx\\n", (int)blockIdx.x, (int)threadIdx.x, bad, val, m);
+    }
+""" + old)
+import re
+n = len(re.findall(r"::WAVE\), s, p\)", s))
+assert n == 1, n
+s = re.sub(r"::WAVE\), s, p\)", "::WAVE) + (DD == 1 ? 16384 : 0), s, p)", s)
+open(p, 'w').write(s)
+PY
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys

@@ -37,6 +37,7 @@
 #include <cstdlib>
 
 #include "fir_kernels.hpp"
+#include "fir_mxi.hpp"
 
 namespace sdrgpu {
 
@@ -273,6 +274,7 @@ struct MxState {
     float* d_taps = nullptr;
     void* d_dummy = nullptr;  // zeroed target of fir_mxh's clamped prefetches
     int tap_scale_exp = 0;    // fir_mxh: 15 - exponent(max |h|)
+    bool taps_finite = true;  // fir_mxi takes integer taps: finite ones only
     int cus = 256;
 };
 
@@ -308,7 +310,10 @@ void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status) {
     st->NCH = mx_nch(K, D);
     {
         float hmax = 0.f;
-        for (int k = 0; k < K; ++k) hmax = std::max(hmax, std::fabs(taps[k]));
+        for (int k = 0; k < K; ++k) {
+            hmax = std::max(hmax, std::fabs(taps[k]));
+            if (!std::isfinite(taps[k])) st->taps_finite = false;
+        }
         int e = 0;
         (void)std::frexp(hmax, &e);
         st->tap_scale_exp = std::min(126, std::max(-126, 15 - e));
@@ -341,8 +346,12 @@ void fir_mx_release(void* state) {
 
 int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     auto* st = static_cast<MxState*>(state);
-    if (st && fp.sample_kind == SDRGPU_CU8) {  // rtl_tcp u8 ingest fused into the fp16 kernel
-        if (fp.D != st->D || fp.K != st->K || !fir_mxh_supported(fp)) return SDRGPU_ERR_UNSUPPORTED;
+    if (st && fp.sample_kind == SDRGPU_CU8) {  // rtl_tcp u8 ingest fused into the FIR load
+        if (fp.D != st->D || fp.K != st->K) return SDRGPU_ERR_UNSUPPORTED;
+        // the int8-MFMA kernel (16-byte aligned channels), else the fp16 one (4-byte aligned)
+        if (st->taps_finite && fir_mxi_supported(fp, st->tap_scale_exp))
+            return fir_mxi_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
+        if (!fir_mxh_supported(fp)) return SDRGPU_ERR_UNSUPPORTED;
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
     }
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
