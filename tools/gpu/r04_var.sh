@@ -7,7 +7,7 @@ O=$R/gpurun_out/${OUT:-r04_var}
 mkdir -p $O
 cd $R
 BUILD=$(echo $VARIANTS | tr " " "\n" | grep -v "^base$" | tr "\n" " ")
-[ -z "$BUILD" ] || MAKEFLAGS=-j16 VARIANTS="$BUILD" timeout -k 10 600 bash tools/experiments/fir_ablate.sh > $O/build.log 2>&1 || { tail -20 $O/build.log; exit 1; }
+[ -z "$BUILD" ] || [ -n "$NOBUILD" ] || MAKEFLAGS=-j16 VARIANTS="$BUILD" timeout -k 10 600 bash tools/experiments/fir_ablate.sh > $O/build.log 2>&1 || { tail -20 $O/build.log; exit 1; }
 for rep in $(seq 1 ${REPS:-3}); do
   for v in prod $VARIANTS; do
     for kind in ${KINDS:-c64}; do
