@@ -290,6 +290,26 @@ assert n == 1, n
 s = re.sub(r"::WAVE\), s, p\)", "::WAVE) + (DD == 1 ? 16384 : 0), s, p)", s)
 open(p, 'w').write(s)
 PY
+  elif [ $part = pkmul ]; then  # the window scale applied with v_pk_mul_f32 (two samples' components per instruction)
+    python3 - $src <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+old = """    unsigned h, l;
+    split2(f.x * sc, f.z * sc, h, l);
+    st32(lds, a, h);
+    st32(lds, a + PLB, l);
+    split2(f.y * sc, f.w * sc, h, l);"""
+assert old in s
+s = s.replace(old, """    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 s2 = {sc, sc};
+    const f32x2 p0 = f32x2{f.x, f.y} * s2, p1 = f32x2{f.z, f.w} * s2;
+    unsigned h, l;
+    split2(p0[0], p1[0], h, l);
+    st32(lds, a, h);
+    st32(lds, a + PLB, l);
+    split2(p0[1], p1[1], h, l);""")
+open(p, 'w').write(s)
+PY
   elif [ $part = wg2 ]; then  # two 4-wave workgroups per CU instead of one 8-wave workgroup
     python3 - $src <<'PY'
 import sys
