@@ -250,10 +250,25 @@ def bench_c2u8(args):
 
     wall, ms = time_events(step, fir.stream(), args.steps, args.warmup,
                            lambda: (fir.sync(), synchronize()))
+    # spot check of the timed outputs (the last step's): the first 4096 and the 4096 outputs
+    # from 2^25 on (the input pattern repeats every 2^22 samples, so that window's input is
+    # the pattern again), against the oracle fed the converted u8 codes
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    worst = 0.0
+    for m0 in (0, 1 << 25):
+        j0 = 4 * m0  # a multiple of the pattern period: the window starts the pattern again
+        hist = pat[-2 * 256:] if j0 else np.full(2 * 256, 128, np.uint8)
+        xin = np.concatenate([hist, pat[:2 * 4 * 4096]])
+        ref = pyoracle.Fir(taps, 4, sample_kind=1).process(pyoracle.u8_to_c64(xin))[64:64 + 4096]
+        got = y.download(4096, offset_bytes=8 * m0)
+        worst = max(worst, float(np.abs(got - ref).max() / np.sqrt(np.mean(np.abs(ref) ** 2))))
+    assert worst <= 1e-5 or args.no_check, worst
     return {"config": "c2u8: configs[1] (255-tap FIR, decim 4) fed from rtl_tcp u8 IQ, "
                       "(v-128)/128 fused into the load, 2^28 samples",
             "metric": "complex Msamples/s (input)", "value": round(n / (ms * 1e-3) / 1e6, 1),
-            "roofline": roof(2 + 8 / 4, n, ms), "wall_ms_per_step": round(wall * 1e3, 3)}
+            "roofline": roof(2 + 8 / 4, n, ms), "wall_ms_per_step": round(wall * 1e3, 3),
+            "kernel": "fir_mxi_kernel<5> (int8 MFMA)", "spot_check_max_over_rms": worst}
 
 
 # ------------------------------------------------------------------------------ c2host

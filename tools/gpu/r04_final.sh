@@ -30,3 +30,12 @@ cut -c1-500 $O/c5_2rank.jsonl
 timeout -k 10 300 python -u bench.py --gpus 2 --no-cpu-baseline --steps 10 --warmup 2 > $O/bench_2rank.jsonl 2> $O/bench_2rank.err || { tail -20 $O/bench_2rank.err; exit 9; }
 cut -c1-300 $O/bench_2rank.jsonl
 fi
+if [ -n "$U8PROF" ]; then  # the u8 ingest launch (fir_mxi): kernel trace + FETCH / WRITE PMC
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_u8 -o run -- python3 $R/bench_configs.py --config c2u8 --steps 20 --warmup 5 > $O/prof_u8.jsonl 2> $O/prof_u8.log || { tail -20 $O/prof_u8.log; exit 10; }
+timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_u8/pmc_fetch -o run -- python3 $R/bench_configs.py --config c2u8 --steps 3 --warmup 1 > $O/pmc_u8_fetch.log 2>&1 || { tail -5 $O/pmc_u8_fetch.log; exit 11; }
+timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_u8/pmc_write -o run -- python3 $R/bench_configs.py --config c2u8 --steps 3 --warmup 1 > $O/pmc_u8_write.log 2>&1 || { tail -5 $O/pmc_u8_write.log; exit 12; }
+cd $R
+python3 tools/pmc_to_json.py $O/pmc_u8 $O/pmc_u8.json fir_mxi && head -8 $O/pmc_u8.json
+cut -c1-400 $O/prof_u8.jsonl
+fi
