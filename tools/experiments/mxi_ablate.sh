@@ -5,6 +5,7 @@
 #   gs2 / gs4 : units of 2 / 4 tiles dealt grid-strided (the c64 headline's dealing)
 #   b4 / b16  : per-workgroup runs of 4 / 16 tiles (product: 8)
 #   w16       : two 8-wave workgroups per CU (4 waves per SIMD, <= 128 VGPRs)
+#   cs2 / cs4 : tiles of 2 / 4 column sets (2 / 4 KiB of raw samples in flight per wave)
 set -e
 cd "$(dirname "$0")/../.."
 mkdir -p tools/experiments/abl
@@ -27,6 +28,8 @@ if v.startswith("gs"):
     rep("seek(cm, (long)blockIdx.x * p.units / gridDim.x + wv);", "seek(cm, (long)blockIdx.x * kWaves + wv);")
 elif v.startswith("b"):
     rep("constexpr int kRunTiles = 8;", "constexpr int kRunTiles = %s;" % v[1:])
+elif v.startswith("cs"):  # cs2 / cs4: 2 / 4 column sets (2 / 4 x 1024 new samples) per staged window
+    rep("constexpr int kCs = 1;", "constexpr int kCs = %s;" % v[2:])
 elif v == "w16":
     rep("__attribute__((amdgpu_waves_per_eu(2, 2)))", "__attribute__((amdgpu_waves_per_eu(4, 4)))")
     rep("std::min((long)cus, ceil_div(p.units, kWaves))", "std::min(2L * cus, ceil_div(p.units, kWaves))")

@@ -47,17 +47,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;  // two waves per SIMD (one workgroup per CU)
 constexpr int kBlock = 64 * kWaves;
-constexpr int kRunTiles = 8;  // per-workgroup runs of 8 tiles (as the fp16 u8 launch)
+constexpr int kCs = 1;        // 256-output column sets per staged window (tile)
+constexpr int kRunTiles = 8;  // per-workgroup runs of 8 x 256 outputs (as the fp16 u8 launch)
 
-template <int NC>
+template <int NC, int CS>
 struct GeoI {
     static constexpr int HR = 64 * NC - 64;       // history samples a tile's window needs
     static constexpr int H = HR;                  // staged history (whole 64-sample rows)
-    static constexpr int WL = H + 1024;           // window samples = bytes per plane
+    static constexpr int TI = 1024 * CS;          // new samples per tile
+    static constexpr int NG = 2 * CS;             // raw groups of 512 samples per tile
+    static constexpr int WL = H + TI;             // window samples = bytes per plane
     static constexpr int WINB = 2 * WL;           // bytes per window buffer (I, Q planes)
     static constexpr int WAVE = 2 * WINB;         // bytes per wave (two buffers)
     static constexpr int HL = 64 - H / 8;         // first lane holding history (8 samples/lane)
-    static_assert(H % 64 == 0 && H >= 64 && H <= 512, "geometry");
+    static_assert(H % 64 == 0 && H >= 64 && H <= 512 && NG + 1 <= CS * NC, "geometry");
 };
 
 struct MxiParams {
@@ -128,11 +131,12 @@ __device__ __forceinline__ void put8(char* lds, int a, const u32x4& w) {
     *reinterpret_cast<uint2*>(lds + a + WL) = im;
 }
 
-template <int NC>
+template <int NC, int CS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxi_kernel(MxiParams p) {
-    using G = GeoI<NC>;
+    using G = GeoI<NC, CS>;
     constexpr int H = G::H, HR = G::HR, WL = G::WL, WINB = G::WINB, HL = G::HL;
+    constexpr int TI = G::TI, NG = G::NG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int lane = threadIdx.x & 63;
@@ -178,9 +182,9 @@ void fir_mxi_kernel(MxiParams p) {
         const int r = v + c;
         rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
     }
-    // staging addresses: lane l stages new samples 8 l + 512 k (k = 0, 1) and, if l >= HL,
-    // history samples 8 (l - HL)
-    const int wa0 = base + win_addr(H + 8 * lane), wa1 = base + win_addr(H + 512 + 8 * lane);
+    // staging addresses: lane l stages new samples 8 l + 512 k (k < NG: the row swizzle is the
+    // same for every k, so group k sits 512 k bytes on) and, if l >= HL, history samples 8 (l - HL)
+    const int wa0 = base + win_addr(H + 8 * lane);
     const int wh = base + win_addr(8 * (lane >= HL ? lane - HL : 0));
 
     // ---- the wave's tile stream (fir_mxh.hip's cursors, per-workgroup blocked units) ----
@@ -189,7 +193,7 @@ void fir_mxi_kernel(MxiParams p) {
         bool ok;
     };
     const long ub1 = ((long)blockIdx.x + 1) * p.units / gridDim.x;
-    auto seek = [&](Cur& c, long u) {
+    auto seek = [&](Cur& c, long u) __attribute__((always_inline)) {
         c.u = u;
         c.t = 0;
         c.ok = u < ub1;
@@ -198,30 +202,30 @@ void fir_mxi_kernel(MxiParams p) {
         c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
         if (c.ok && c.nt <= 0) c.ok = false;
     };
-    auto adv = [&](Cur& c) {
+    auto adv = [&](Cur& c) __attribute__((always_inline)) {
         if (!c.ok) return;
         if (++c.t >= c.nt) seek(c, c.u + kWaves);
     };
     const long n_in = p.n_in;
-    auto tile_j0 = [&](const Cur& c) { return 1024L * (c.tu + c.t); };
-    auto tile_fast = [&](const Cur& c) { return 1024L * (c.tu + c.t + 1) <= n_in; };
+    auto tile_j0 = [&](const Cur& c) { return (long)TI * (c.tu + c.t); };
+    auto tile_fast = [&](const Cur& c) { return (long)TI * (c.tu + c.t + 1) <= n_in; };
     auto chan = [&](const Cur& c) { return p.in + 2 * c.ch * p.ld_in; };
-    auto load_tile = [&](u32x4 (&dst)[2], const Cur& c) {
+    auto load_tile = [&](u32x4 (&dst)[NG], const Cur& c) __attribute__((always_inline)) {
         const long j0 = tile_j0(c);
         if (tile_fast(c)) {
             const u32x4* q = reinterpret_cast<const u32x4*>(chan(c) + 2 * j0);
-            dst[0] = __builtin_nontemporal_load(q + lane);
-            dst[1] = __builtin_nontemporal_load(q + 64 + lane);
+#pragma unroll
+            for (int k = 0; k < NG; ++k) dst[k] = __builtin_nontemporal_load(q + 64 * k + lane);
         } else {
             asm volatile("" ::: "memory");
             const unsigned short* in = reinterpret_cast<const unsigned short*>(chan(c));
             const float2* hist = p.hist + c.ch * (long)(K - 1);
-            dst[0] = fetch8(in, hist, j0 + 8 * lane, n_in, K);
-            dst[1] = fetch8(in, hist, j0 + 512 + 8 * lane, n_in, K);
+#pragma unroll
+            for (int k = 0; k < NG; ++k) dst[k] = fetch8(in, hist, j0 + 512 * k + 8 * lane, n_in, K);
         }
     };
     // the H samples before tile c, 8 per lane in lanes HL..63 (the tail layout of a raw tile)
-    auto load_hist = [&](u32x4& dst, const Cur& c) {
+    auto load_hist = [&](u32x4& dst, const Cur& c) __attribute__((always_inline)) {
         const long j = tile_j0(c) - H + 8 * (lane >= HL ? lane - HL : 0);
         if (tile_j0(c) >= H && tile_j0(c) <= n_in) {
             dst = *reinterpret_cast<const u32x4*>(chan(c) + 2 * j);
@@ -235,23 +239,23 @@ void fir_mxi_kernel(MxiParams p) {
     Cur cm, st, ld;
     seek(cm, (long)blockIdx.x * p.units / gridDim.x + wv);
     if (cm.ok) {
-        u32x4 nx[2], hr;
+        u32x4 nx[NG], hr;
         load_hist(hr, cm);
         load_tile(nx, cm);
         if (lane >= HL) put8<WL>(smem, wh, hr);
-        put8<WL>(smem, wa0, nx[0]);
-        put8<WL>(smem, wa1, nx[1]);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) put8<WL>(smem, wa0 + 512 * k, nx[k]);
         st = cm;
         adv(st);
         if (st.ok && st.t == 0) load_hist(hr, st);
-        else hr = nx[1];
+        else hr = nx[NG - 1];
         if (st.ok) load_tile(nx, st);
         ld = st;
         adv(ld);
 
         const float sc0 = __builtin_amdgcn_ldexpf(1.0f, -(p.S + 7));
         const float sc1 = sc0 * 256.0f, sc2 = sc0 * 65536.0f;
-        auto body = [&](auto tau_c) {
+        auto body = [&](auto tau_c) __attribute__((always_inline)) {
             constexpr int TAU = decltype(tau_c)::value;
             constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
             const bool fast2 = ld.ok && tile_fast(ld);
@@ -259,70 +263,74 @@ void fir_mxi_kernel(MxiParams p) {
             const u32x4* src2 = reinterpret_cast<const u32x4*>(
                 fast2 ? chan(ld) + 2 * tile_j0(ld) : p.dummy);
             i32x4 acc[2][3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) acc[0][d] = acc[1][d] = i32x4{0, 0, 0, 0};
             u32x4 fb[2][2];
-            auto read_frags = [&](u32x4 (&f)[2], int c) {
-                const int a = rb[c] + TAU * WINB;
+            // column set j reads 1024 samples (16 rows, the same swizzle) further into the window
+            auto read_frags = [&](u32x4 (&f)[2], int i) __attribute__((always_inline)) {
+                const int a = rb[i % NC] + TAU * WINB + 1024 * (i / NC);
                 f[0] = *reinterpret_cast<const u32x4*>(smem + a);
                 f[1] = *reinterpret_cast<const u32x4*>(smem + a + WL);
             };
             read_frags(fb[0], 0);
-            u32x4 keep = nx[1];
+            const u32x4 keep = nx[NG - 1];
+            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                if (c + 1 < NC) read_frags(fb[(c + 1) & 1], c + 1);
+            for (int i = 0; i < CS * NC; ++i) {
+                const int j = i / NC, c = i % NC;
+                if (c == 0) {
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) acc[0][d] = acc[1][d] = i32x4{0, 0, 0, 0};
+                }
+                if (i + 1 < CS * NC) read_frags(fb[(i + 1) & 1], i + 1);
                 __builtin_amdgcn_sched_barrier(0);
-                const u32x4(&f)[2] = fb[c & 1];
+                const u32x4(&f)[2] = fb[i & 1];
 #pragma unroll
                 for (int d = 2; d >= 0; --d) {
                     acc[0][d] = mfma8(ad[c][d], f[0], acc[0][d]);
                     acc[1][d] = mfma8(ad[c][d], f[1], acc[1][d]);
                 }
-                if (c == 0) {  // window k+1's history; then tile k+2's, if it opens a run
+                if (i == 0) {  // window k+1's history; then tile k+2's, if it opens a run
                     if (lane >= HL) put8<WL>(smem, WN + wh, hr);
                     if (ld_run) load_hist(hr, ld);
                 }
-                if (c == 1) {
-                    put8<WL>(smem, WN + wa0, nx[0]);
-                    nx[0] = __builtin_nontemporal_load(src2 + lane);
+#pragma unroll
+                for (int k = 0; k < NG; ++k) {
+                    if (k + 1 != i) continue;
+                    put8<WL>(smem, WN + wa0 + 512 * k, nx[k]);
+                    nx[k] = __builtin_nontemporal_load(src2 + 64 * k + lane);
                 }
-                if (c == 2) {
-                    put8<WL>(smem, WN + wa1, nx[1]);
-                    nx[1] = __builtin_nontemporal_load(src2 + 64 + lane);
+                if (c == NC - 1) {  // column set j complete: scale and store its 256 outputs
+                    const long m0 = (cm.tu + cm.t) * (256L * CS) + 256 * j;
+                    const long m = m0 + 16 * v + 4 * g;
+                    float yr[4], yi[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        yr[q] = fmaf((float)acc[0][2][q], sc2, fmaf((float)acc[0][1][q], sc1, (float)acc[0][0][q] * sc0));
+                        yi[q] = fmaf((float)acc[1][2][q], sc2, fmaf((float)acc[1][1][q], sc1, (float)acc[1][0][q] * sc0));
+                    }
+                    if (p.vec_out && m0 + 256 <= p.n_out) {
+                        // line-complete stores (fir_mxh.hip): lanes v and v^1 swap one 16-B half
+                        const bool ev = (v & 1) == 0;
+                        const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                        const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                        f32x4 rx;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
+                                __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
+                        const long mp = m0 + 16 * (v ^ 1) + 4 * g;
+                        f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
+                        f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
+                        __builtin_nontemporal_store(ev ? y0 : rx, o4);
+                        __builtin_nontemporal_store(ev ? rx : y1, p4);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (m + q < p.n_out) out[m + q] = make_float2(yr[q], yi[q]);
+                    }
                 }
             }
             if (!ld_run) hr = keep;  // tile k+2 continues the run: its history is k+1's tail
             if (!fast2 && ld.ok) load_tile(nx, ld);
-            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            const long m0 = (cm.tu + cm.t) * 256;
-            const long m = m0 + 16 * v + 4 * g;
-            float yr[4], yi[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                yr[i] = fmaf((float)acc[0][2][i], sc2, fmaf((float)acc[0][1][i], sc1, (float)acc[0][0][i] * sc0));
-                yi[i] = fmaf((float)acc[1][2][i], sc2, fmaf((float)acc[1][1][i], sc1, (float)acc[1][0][i] * sc0));
-            }
-            if (p.vec_out && m0 + 256 <= p.n_out) {
-                // line-complete stores (fir_mxh.hip): lanes v and v^1 swap one 16-B half
-                const bool ev = (v & 1) == 0;
-                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                f32x4 rx;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
-                        __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
-                const long mp = m0 + 16 * (v ^ 1) + 4 * g;
-                f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
-                f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
-                __builtin_nontemporal_store(ev ? y0 : rx, o4);
-                __builtin_nontemporal_store(ev ? rx : y1, p4);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
-            }
             cm = st;
             st = ld;
             adv(ld);
@@ -389,17 +397,17 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    p.tpc = ceil_div(std::max(0L, fp.n_out), 256L);
-    p.seg_tiles = std::max(1L, std::min<long>(kRunTiles, p.tpc));
+    p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * kCs);
+    p.seg_tiles = std::max(1L, std::min<long>(std::max(1, kRunTiles / kCs), p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
     if (NC == 5)
-        hipLaunchKernelGGL((fir_mxi_kernel<5>), dim3(blocks), dim3(kBlock),
-                           (size_t)kWaves * GeoI<5>::WAVE, s, p);
+        hipLaunchKernelGGL((fir_mxi_kernel<5, kCs>), dim3(blocks), dim3(kBlock),
+                           (size_t)kWaves * (GeoI<5, kCs>::WAVE), s, p);
     else
-        hipLaunchKernelGGL((fir_mxi_kernel<3>), dim3(blocks), dim3(kBlock),
-                           (size_t)kWaves * GeoI<3>::WAVE, s, p);
+        hipLaunchKernelGGL((fir_mxi_kernel<3, kCs>), dim3(blocks), dim3(kBlock),
+                           (size_t)kWaves * (GeoI<3, kCs>::WAVE), s, p);
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }
