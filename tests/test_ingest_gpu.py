@@ -142,3 +142,20 @@ def test_cu8_tap_scale_range(sdr, oracle, scale):
     y = f.process(raw)
     ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
     assert_parity(y, ref, what=f"tap scale {scale}")
+
+
+@pytest.mark.parametrize("K", [2, 64, 65, 129, 130, 193, 257, 258])
+def test_cu8_int8_tap_count_boundaries(sdr, oracle, K):
+    """Tap counts at the int8 kernel's chunk boundaries (3 K = 64 chunks up to K = 129, 5 up to
+    257; 258 takes the converting path), over ragged blocks so every decimation phase and a
+    partial last tile occur, and the stream history (K - 1 converted samples) is carried."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(1000 + K)
+    taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+    n = 3 * 1024 + 777
+    raw = u8_stream(rng, n)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
+    f = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+    cuts = [0, 1, 1030, 1031, 2053, n]
+    y = np.concatenate([f.process(raw[2 * a:2 * b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    assert_parity(y, ref, what=f"K {K}")
