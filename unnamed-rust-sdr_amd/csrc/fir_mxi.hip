@@ -12,7 +12,7 @@
 // digits t = 2^16 d2 + 2^8 d1 + d0.  v_mfma_i32_16x16x64_i8 then sums digit x sample
 // products exactly in i32 (|sum| <= 5 x 64 x 128^2 < 2^23 per digit), and the tile's outputs
 // are (2^16 C2 + 2^8 C1 + C0) 2^-(S+7) with two f32 roundings -- the one approximation is the
-// taps' 23-bit rounding (fp16 kernel: 22 bits).
+// taps' rounding to integers, <= 2^-22 of max |h| (the fp16 kernel's hh + hl: about the same).
 //
 // Against the fp16 form of the same tiles (fir_mxh.hip, U8 = true): K = 64 per MFMA at the
 // same 16 cycles, so 3 digits x 5 chunks x 2 components = 30 MFMAs per 256-output tile
