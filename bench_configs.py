@@ -252,13 +252,15 @@ def bench_c2u8(args):
                            lambda: (fir.sync(), synchronize()))
     # spot check of the timed outputs (the last step's): the first 4096 and the 4096 outputs
     # from 2^25 on (the input pattern repeats every 2^22 samples, so that window's input is
-    # the pattern again), against the oracle fed the converted u8 codes
+    # the pattern again), against the oracle fed the converted u8 codes.  The handle streams:
+    # the last step's history is the end of the step before it (the pattern's tail again).
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     worst = 0.0
     for m0 in (0, 1 << 25):
         j0 = 4 * m0  # a multiple of the pattern period: the window starts the pattern again
-        hist = pat[-2 * 256:] if j0 else np.full(2 * 256, 128, np.uint8)
+        first_call = j0 == 0 and args.steps + args.warmup == 1
+        hist = np.full(2 * 256, 128, np.uint8) if first_call else pat[-2 * 256:]
         xin = np.concatenate([hist, pat[:2 * 4 * 4096]])
         ref = pyoracle.Fir(taps, 4, sample_kind=1).process(pyoracle.u8_to_c64(xin))[64:64 + 4096]
         got = y.download(4096, offset_bytes=8 * m0)

@@ -11,6 +11,7 @@ if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 fi
+if [ -z "$SKIP_HEAD" ]; then
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 2; }
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jsonl 2> $O/bench.err || { tail -20 $O/bench.err; exit 3; }
@@ -22,6 +23,7 @@ timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc/pmc_f
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc/pmc_write -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-channel-sharded > $O/pmc_write.log 2>&1 || { tail -5 $O/pmc_write.log; exit 6; }
 cd $R
 python3 tools/pmc_to_json.py $O/pmc $O/pmc_fir_c2.json fir_mxh && head -8 $O/pmc_fir_c2.json
+fi
 if [ -z "$SKIP_CONFIGS" ]; then
 timeout -k 10 900 python -u bench_configs.py > $O/configs.jsonl 2> $O/configs.err || { tail -20 $O/configs.err; exit 7; }
 cut -c1-300 $O/configs.jsonl
