@@ -1,5 +1,5 @@
-// fir_mxi.hip -- rtl_tcp u8 I/Q FIR decimate by 4 on the int8 MFMAs (gfx950): the fused
-// ingest of SURVEY 8f-1 with exact integer products.
+// fir_mxi.hip -- rtl_tcp u8 I/Q FIR (decimate by 4, or no decimation) on the int8 MFMAs
+// (gfx950): the fused ingest of SURVEY 8f-1 with exact integer products.
 //
 // Semantics: RtlTcpSignal::next (reference src/rtltcp.rs:156-164: x = (v - 128) / 128) feeding
 // Fir::apply + Decimate (src/filter/fir.rs:23-32, src/filter/convolve.rs:13-15,
@@ -25,6 +25,11 @@
 // registers) and columns v = the tile's 16 blocks (B = samples: B[p][v] = window[64 v + p]);
 // K = 320 window samples = 5 chunks of 64 (H = 256 history samples).
 //
+// D = 1 (the same stream without Decimate): rows are 16 consecutive outputs, columns blocks
+// 16 samples apart, K = 5 chunks cover K + 15 <= 320; a tile is four 256-output column sets
+// over one staged window of H + 1024 samples (so the raw-tile pipeline is the D = 4 one), and
+// the LDS layout is linear (conflict free for that block spacing).
+//
 // LDS (wave-private, no barriers): two window buffers (compute tile k from one while tile
 // k + 1 is staged into the other), each two planes (I, Q) of H + 1024 int8 samples in rows of
 // 64 B; window sample b sits at 64 (b >> 6) + 16 (((b >> 4) & 3) ^ ((b >> 7) & 3)) + (b & 15).
@@ -47,20 +52,23 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;  // two waves per SIMD (one workgroup per CU)
 constexpr int kBlock = 64 * kWaves;
-constexpr int kCs = 1;        // 256-output column sets per staged window (tile)
+constexpr int kCs = 1;        // D = 4: 256-output column sets per staged window (tile)
+constexpr int kCs1 = 4;       // D = 1: four sets, so a tile is 1024 new samples as at D = 4
 constexpr int kRunTiles = 8;  // per-workgroup runs of 8 x 256 outputs (as the fp16 u8 launch)
 
-template <int NC, int CS>
+template <int NC, int CS, int D>
 struct GeoI {
-    static constexpr int HR = 64 * NC - 64;       // history samples a tile's window needs
-    static constexpr int H = HR;                  // staged history (whole 64-sample rows)
-    static constexpr int TI = 1024 * CS;          // new samples per tile
-    static constexpr int NG = 2 * CS;             // raw groups of 512 samples per tile
+    static constexpr int HR = 64 * NC - 16 * D;   // history samples a tile's window needs
+    static constexpr int H = (HR + 63) / 64 * 64; // staged history (whole 64-sample rows)
+    static constexpr int OFF = H - HR;            // window offset inside the buffer
+    static constexpr int TI = 256 * D * CS;       // new samples per tile
+    static constexpr int NG = TI / 512;           // raw groups of 512 samples per tile
     static constexpr int WL = H + TI;             // window samples = bytes per plane
     static constexpr int WINB = 2 * WL;           // bytes per window buffer (I, Q planes)
     static constexpr int WAVE = 2 * WINB;         // bytes per wave (two buffers)
     static constexpr int HL = 64 - H / 8;         // first lane holding history (8 samples/lane)
-    static_assert(H % 64 == 0 && H >= 64 && H <= 512 && NG + 1 <= CS * NC, "geometry");
+    static_assert(TI % 512 == 0 && H <= 512 && NG + 1 <= CS * NC, "geometry");
+    static_assert(D == 1 || (D == 4 && OFF == 0), "geometry");
 };
 
 struct MxiParams {
@@ -71,7 +79,7 @@ struct MxiParams {
     const unsigned char* dummy;  // >= 2 KiB readable: target of clamped prefetches
     long n_out;
     int K;
-    int delta;  // 3 - i0
+    int delta;  // D - 1 - i0
     int S;      // taps scaled by 2^S before the digit split
     const float* taps;
     float2* out;
@@ -112,8 +120,11 @@ __device__ __forceinline__ u32x4 fetch8(const unsigned short* in, const float2* 
     return r;
 }
 
-// window sample b -> byte offset inside a plane
+// window sample b -> byte offset inside a plane: D = 4 swizzles 16-byte units within 64-byte
+// rows; at D = 1 (blocks 16 samples apart) the linear layout is already conflict free
+template <int D>
 __device__ __forceinline__ int win_addr(int b) {
+    if constexpr (D == 1) return b;
     return 64 * (b >> 6) + 16 * (((b >> 4) & 3) ^ ((b >> 7) & 3)) + (b & 15);
 }
 
@@ -131,10 +142,10 @@ __device__ __forceinline__ void put8(char* lds, int a, const u32x4& w) {
     *reinterpret_cast<uint2*>(lds + a + WL) = im;
 }
 
-template <int NC, int CS>
+template <int NC, int CS, int D>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxi_kernel(MxiParams p) {
-    using G = GeoI<NC, CS>;
+    using G = GeoI<NC, CS, D>;
     constexpr int H = G::H, HR = G::HR, WL = G::WL, WINB = G::WINB, HL = G::HL;
     constexpr int TI = G::TI, NG = G::NG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -158,7 +169,7 @@ void fir_mxi_kernel(MxiParams p) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int pidx = 64 * c + 16 * g + 4 * q + e;
-                    const int k = 4 * v + 3 - p.delta + HR - pidx;
+                    const int k = D * v + D - 1 - p.delta + HR - pidx;
                     const bool ok = (k >= 0) & (k < K);
                     const float hk = p.taps[ok ? k : 0];
                     const int t = ok ? (int)rintf(hk * tsc) : 0;
@@ -179,13 +190,17 @@ void fir_mxi_kernel(MxiParams p) {
     int rb[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        const int r = v + c;
-        rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
+        if constexpr (D == 4) {
+            const int r = v + c;
+            rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
+        } else {
+            rb[c] = base + G::OFF + 16 * v + 64 * c + 16 * g;
+        }
     }
     // staging addresses: lane l stages new samples 8 l + 512 k (k < NG: the row swizzle is the
     // same for every k, so group k sits 512 k bytes on) and, if l >= HL, history samples 8 (l - HL)
-    const int wa0 = base + win_addr(H + 8 * lane);
-    const int wh = base + win_addr(8 * (lane >= HL ? lane - HL : 0));
+    const int wa0 = base + win_addr<D>(H + 8 * lane);
+    const int wh = base + win_addr<D>(8 * (lane >= HL ? lane - HL : 0));
 
     // ---- the wave's tile stream (fir_mxh.hip's cursors, per-workgroup blocked units) ----
     struct Cur {
@@ -264,9 +279,10 @@ void fir_mxi_kernel(MxiParams p) {
                 fast2 ? chan(ld) + 2 * tile_j0(ld) : p.dummy);
             i32x4 acc[2][3];
             u32x4 fb[2][2];
-            // column set j reads 1024 samples (16 rows, the same swizzle) further into the window
+            // column set j reads 256 D samples further into the window (D = 4: 16 rows, the
+            // same swizzle)
             auto read_frags = [&](u32x4 (&f)[2], int i) __attribute__((always_inline)) {
-                const int a = rb[i % NC] + TAU * WINB + 1024 * (i / NC);
+                const int a = rb[i % NC] + TAU * WINB + 256 * D * (i / NC);
                 f[0] = *reinterpret_cast<const u32x4*>(smem + a);
                 f[1] = *reinterpret_cast<const u32x4*>(smem + a + WL);
             };
@@ -355,16 +371,17 @@ void fir_mxi_kernel(MxiParams p) {
     }
 }
 
-int mxi_nc(int K) {
-    const int need = (K + 63 + 63) / 64;  // 64 NC >= K + 15*4 + 3
+int mxi_nc(int K, int D) {
+    const int need = (K + 16 * D - 1 + 63) / 64;  // 64 NC >= K + 15 D + D - 1
     return need <= 3 ? 3 : (need <= 5 ? 5 : 0);
 }
 
 }  // namespace
 
 int fir_mxi_supported(const FirParams& fp, int tap_scale_exp) {
-    if (fp.sample_kind != SDRGPU_CU8 || fp.tap_kind != SDRGPU_F32 || fp.D != 4) return 0;
-    if (fp.K < 1 || mxi_nc(fp.K) == 0 || fp.i0 < 0 || fp.i0 >= 4) return 0;
+    if (fp.sample_kind != SDRGPU_CU8 || fp.tap_kind != SDRGPU_F32) return 0;
+    if (!(fp.D == 4 || fp.D == 1) || fp.K < 1 || fp.K > 257) return 0;
+    if (mxi_nc(fp.K, fp.D) == 0 || fp.i0 < 0 || fp.i0 >= fp.D) return 0;
     // taps as 23-bit integers: 2^S and the output scale 2^-(S + 7) stay normal floats
     if (tap_scale_exp + 14 > 126 || tap_scale_exp + 7 < -126) return 0;
     // 16-byte loads of 8 samples: channel bases stay 16-byte aligned
@@ -377,7 +394,8 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                    const void* d_dummy, int cus, hipStream_t s) {
     if (!fir_mxi_supported(fp, tap_scale_exp) || !d_dummy || fir_mxh_dummy_bytes() < 2048)
         return SDRGPU_ERR_UNSUPPORTED;
-    const int NC = mxi_nc(fp.K);
+    const int D = fp.D;
+    const int NC = mxi_nc(fp.K, D);
     MxiParams p;
     p.in = static_cast<const unsigned char*>(fp.in);
     p.ld_in = fp.ld_in;
@@ -387,7 +405,7 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     p.dummy = static_cast<const unsigned char*>(d_dummy);
     p.n_out = fp.n_out;
     p.K = fp.K;
-    p.delta = (int)(3 - fp.i0);
+    p.delta = (int)(D - 1 - fp.i0);
     p.S = tap_scale_exp + 7;
     p.taps = d_taps;
     p.out = static_cast<float2*>(fp.out);
@@ -397,17 +415,20 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * kCs);
-    p.seg_tiles = std::max(1L, std::min<long>(std::max(1, kRunTiles / kCs), p.tpc));
+    const int cs = D == 4 ? kCs : kCs1;
+    p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
+    p.seg_tiles = std::max(1L, std::min<long>(std::max(1, kRunTiles / cs), p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
-    if (NC == 5)
-        hipLaunchKernelGGL((fir_mxi_kernel<5, kCs>), dim3(blocks), dim3(kBlock),
-                           (size_t)kWaves * (GeoI<5, kCs>::WAVE), s, p);
-    else
-        hipLaunchKernelGGL((fir_mxi_kernel<3, kCs>), dim3(blocks), dim3(kBlock),
-                           (size_t)kWaves * (GeoI<3, kCs>::WAVE), s, p);
+#define SDRGPU_MXI_GO(NCC, CSS, DD)                                                            \
+    hipLaunchKernelGGL((fir_mxi_kernel<NCC, CSS, DD>), dim3(blocks), dim3(kBlock),             \
+                       (size_t)kWaves * (GeoI<NCC, CSS, DD>::WAVE), s, p)
+    if (D == 4 && NC == 5) SDRGPU_MXI_GO(5, kCs, 4);
+    else if (D == 4) SDRGPU_MXI_GO(3, kCs, 4);
+    else if (NC == 5) SDRGPU_MXI_GO(5, kCs1, 1);
+    else SDRGPU_MXI_GO(3, kCs1, 1);
+#undef SDRGPU_MXI_GO
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }
