@@ -298,7 +298,11 @@ void fir_mxh_kernel(MxhParams p) {
         c.u = u;
         c.t = 0;
         c.ok = u < ub1;
-        c.ch = c.ok ? u / p.spc : 0;
+        if constexpr (D == 4 && !U8) {  // one stream (the headline): no 64-bit division per unit
+            c.ch = c.ok && p.spc < p.units ? u / p.spc : 0;
+        } else {
+            c.ch = c.ok ? u / p.spc : 0;
+        }
         c.tu = (u - c.ch * p.spc) * p.seg_tiles;
         c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
         if (c.ok && c.nt <= 0) c.ok = false;  // (units past a channel's last tile: none by construction)
