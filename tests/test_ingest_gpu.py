@@ -161,25 +161,27 @@ def test_cu8_int8_tap_count_boundaries(sdr, oracle, K):
     assert_parity(y, ref, what=f"K {K}")
 
 
-@pytest.mark.parametrize("K", [1, 64, 177, 178, 255, 257])
-def test_cu8_int8_no_decimation(sdr, oracle, K):
-    """D = 1 u8 blocks on the int8 kernel (four 256-output column sets per 1024-sample tile,
-    linear LDS): chunk-count boundary K = 177 / 178, ragged blocks, a partial last tile, then a
-    3-channel bank whose leading dimension keeps the 16-byte alignment."""
+@pytest.mark.parametrize("D,K", [(1, 1), (1, 64), (1, 177), (1, 178), (1, 255), (1, 257),
+                                 (2, 1), (2, 161), (2, 162), (2, 255), (2, 257)])
+def test_cu8_int8_no_decimation(sdr, oracle, D, K):
+    """D = 1 and 2 u8 blocks on the int8 kernel (4 / D 256-output column sets per 1024-sample
+    tile, linear LDS): chunk-count boundaries (K = 177 / 178 at D = 1, 161 / 162 at D = 2),
+    ragged blocks (every decimation phase), a partial last tile, then a 3-channel bank whose
+    leading dimension keeps the 16-byte alignment."""
     from sdrgpu import _lib
-    rng = np.random.default_rng(2000 + K)
+    rng = np.random.default_rng(2000 + K + 7 * D)
     taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
     n = 5 * 1024 + 333
     raw = u8_stream(rng, n)
-    ref = oracle.Fir(taps, 1, sample_kind=1).process(oracle.u8_to_c64(raw))
-    f = sdr.filter.Fir(taps, decim=1, sample_kind=_lib.CU8).design(2.4e6)
+    ref = oracle.Fir(taps, D, sample_kind=1).process(oracle.u8_to_c64(raw))
+    f = sdr.filter.Fir(taps, decim=D, sample_kind=_lib.CU8).design(2.4e6)
     cuts = [0, 5, 1029, 2048, 4100, n]
     y = np.concatenate([f.process(raw[2 * a:2 * b]) for a, b in zip(cuts[:-1], cuts[1:])])
     assert f.last_algorithm() == _lib.FIR_MATRIX
     assert_parity(y, ref, what=f"K {K}")
     nch, nb = 3, 4096 + 8
     x = rng.integers(0, 256, size=(nch, 2 * nb), dtype=np.uint8)
-    yb = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=1).process(x)
+    yb = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=D).process(x)
     for c in range(nch):
-        assert_parity(yb[c], oracle.Fir(taps, 1, sample_kind=1).process(oracle.u8_to_c64(x[c])),
+        assert_parity(yb[c], oracle.Fir(taps, D, sample_kind=1).process(oracle.u8_to_c64(x[c])),
                       what=f"bank K {K} ch {c}")

@@ -25,10 +25,10 @@
 // registers) and columns v = the tile's 16 blocks (B = samples: B[p][v] = window[64 v + p]);
 // K = 320 window samples = 5 chunks of 64 (H = 256 history samples).
 //
-// D = 1 (the same stream without Decimate): rows are 16 consecutive outputs, columns blocks
-// 16 samples apart, K = 5 chunks cover K + 15 <= 320; a tile is four 256-output column sets
-// over one staged window of H + 1024 samples (so the raw-tile pipeline is the D = 4 one), and
-// the LDS layout is linear (conflict free for that block spacing).
+// D = 1 (the same stream without Decimate) and D = 2: rows are 16 outputs D samples apart,
+// columns blocks 16 D samples apart, K = 5 chunks cover K + 15 D + D - 1 <= 320; a tile is
+// 4 / D 256-output column sets over one staged window of H + 1024 samples (so the raw-tile
+// pipeline is the D = 4 one), and the LDS layout is linear (conflict free for those spacings).
 //
 // LDS (wave-private, no barriers): two window buffers (compute tile k from one while tile
 // k + 1 is staged into the other), each two planes (I, Q) of H + 1024 int8 samples in rows of
@@ -54,6 +54,7 @@ constexpr int kWaves = 8;  // two waves per SIMD (one workgroup per CU)
 constexpr int kBlock = 64 * kWaves;
 constexpr int kCs = 1;        // D = 4: 256-output column sets per staged window (tile)
 constexpr int kCs1 = 4;       // D = 1: four sets, so a tile is 1024 new samples as at D = 4
+constexpr int kCs2 = 2;       // D = 2: two sets
 constexpr int kRunTiles = 8;  // per-workgroup runs of 8 x 256 outputs (as the fp16 u8 launch)
 
 template <int NC, int CS, int D>
@@ -68,7 +69,7 @@ struct GeoI {
     static constexpr int WAVE = 2 * WINB;         // bytes per wave (two buffers)
     static constexpr int HL = 64 - H / 8;         // first lane holding history (8 samples/lane)
     static_assert(TI % 512 == 0 && H <= 512 && NG + 1 <= CS * NC, "geometry");
-    static_assert(D == 1 || (D == 4 && OFF == 0), "geometry");
+    static_assert(D != 4 || OFF == 0, "geometry");
 };
 
 struct MxiParams {
@@ -121,10 +122,10 @@ __device__ __forceinline__ u32x4 fetch8(const unsigned short* in, const float2* 
 }
 
 // window sample b -> byte offset inside a plane: D = 4 swizzles 16-byte units within 64-byte
-// rows; at D = 1 (blocks 16 samples apart) the linear layout is already conflict free
+// rows; at D = 1 and 2 (blocks 16 / 32 samples apart) the linear layout is already conflict free
 template <int D>
 __device__ __forceinline__ int win_addr(int b) {
-    if constexpr (D == 1) return b;
+    if constexpr (D != 4) return b;
     return 64 * (b >> 6) + 16 * (((b >> 4) & 3) ^ ((b >> 7) & 3)) + (b & 15);
 }
 
@@ -194,7 +195,7 @@ void fir_mxi_kernel(MxiParams p) {
             const int r = v + c;
             rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
         } else {
-            rb[c] = base + G::OFF + 16 * v + 64 * c + 16 * g;
+            rb[c] = base + G::OFF + 16 * D * v + 64 * c + 16 * g;
         }
     }
     // staging addresses: lane l stages new samples 8 l + 512 k (k < NG: the row swizzle is the
@@ -380,7 +381,7 @@ int mxi_nc(int K, int D) {
 
 int fir_mxi_supported(const FirParams& fp, int tap_scale_exp) {
     if (fp.sample_kind != SDRGPU_CU8 || fp.tap_kind != SDRGPU_F32) return 0;
-    if (!(fp.D == 4 || fp.D == 1) || fp.K < 1 || fp.K > 257) return 0;
+    if (!(fp.D == 4 || fp.D == 2 || fp.D == 1) || fp.K < 1 || fp.K > 257) return 0;
     if (mxi_nc(fp.K, fp.D) == 0 || fp.i0 < 0 || fp.i0 >= fp.D) return 0;
     // taps as 23-bit integers: 2^S and the output scale 2^-(S + 7) stay normal floats
     if (tap_scale_exp + 14 > 126 || tap_scale_exp + 7 < -126) return 0;
@@ -415,7 +416,7 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    const int cs = D == 4 ? kCs : kCs1;
+    const int cs = D == 4 ? kCs : (D == 2 ? kCs2 : kCs1);
     p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     p.seg_tiles = std::max(1L, std::min<long>(std::max(1, kRunTiles / cs), p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
@@ -426,6 +427,8 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                        (size_t)kWaves * (GeoI<NCC, CSS, DD>::WAVE), s, p)
     if (D == 4 && NC == 5) SDRGPU_MXI_GO(5, kCs, 4);
     else if (D == 4) SDRGPU_MXI_GO(3, kCs, 4);
+    else if (D == 2 && NC == 5) SDRGPU_MXI_GO(5, kCs2, 2);
+    else if (D == 2) SDRGPU_MXI_GO(3, kCs2, 2);
     else if (NC == 5) SDRGPU_MXI_GO(5, kCs1, 1);
     else SDRGPU_MXI_GO(3, kCs1, 1);
 #undef SDRGPU_MXI_GO
