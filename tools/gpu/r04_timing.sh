@@ -2,6 +2,9 @@
 # Round 4: the driver's bench command with one event pair around the timed launches (now) vs
 # an event pair around every launch (--event-per-launch, rounds 1-4), alternating, then a
 # rocprofv3 kernel trace of the driver's command (gaps between the timed launches).
+# Ran against a bench.py with the one-pair timing and an --event-per-launch flag (round 4);
+# the one-pair variant was not kept, so bench.py has neither the mode nor the flag now
+# (result: profiles/r04_bench_timing_ab.txt).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r04_timing}
