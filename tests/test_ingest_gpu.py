@@ -185,3 +185,52 @@ def test_cu8_int8_no_decimation(sdr, oracle, D, K):
     for c in range(nch):
         assert_parity(yb[c], oracle.Fir(taps, D, sample_kind=1).process(oracle.u8_to_c64(x[c])),
                       what=f"bank K {K} ch {c}")
+
+
+@pytest.mark.slow
+def test_cu8_full_size_configs1_properties(sdr, oracle):
+    """configs[1] fed from rtl_tcp u8 at full size (2^28 samples, the int8 kernel): windows at
+    the stream ends, at per-workgroup unit boundaries and at random places against the oracle;
+    then the whole stream again as two ragged blocks -- the int8 kernel sums exact integers,
+    so its outputs do not depend on where tiles and blocks fall: array_equal over all 2^26."""
+    from sdrgpu import _lib
+    from sdrgpu.device import DeviceBuffer
+    import scipy.signal as ss
+    n = 1 << 28
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    dx = DeviceBuffer.empty(2 * n, np.uint8)
+    chunk = 1 << 25
+    for i in range(0, 2 * n, chunk):
+        dx.upload(np.random.default_rng(300 + i // chunk).integers(0, 256, chunk, dtype=np.uint8),
+                  offset_bytes=i)
+    n_out = n // 4
+    f = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+    dy = DeviceBuffer.empty(n_out, np.complex64)
+    assert f.process_dev(dx.ptr, n, dy.ptr, n_out) == n_out
+    f.sync()
+    rng = np.random.default_rng(1)
+    # units: runs of 8 tiles of 256 outputs, 2048-output steps; a workgroup's range ends at
+    # units * b / 256 for b = 1 .. 255 (fir_mxi_launch's blocked dealing at 256 CUs)
+    units = n_out // 2048
+    edges = [2048 * (units * b // 256) for b in (1, 97, 255)]
+    starts = [0, n_out - 4096] + [e - 2048 for e in edges] + [int(v) for v in rng.integers(1, n_out - 4096, 4)]
+    for m0 in starts:
+        g0 = max(0, 4 * m0 - 256)
+        g1 = 4 * (m0 + 4096)
+        raw = dx.download(2 * (g1 - g0), dtype=np.uint8, offset_bytes=2 * g0)
+        ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
+        skip = m0 - g0 // 4
+        assert_parity(dy.download(4096, offset_bytes=8 * m0), ref[skip:skip + 4096],
+                      what=f"window {m0}")
+    cut = 123456789  # ragged: not a tile, unit or decimation-phase boundary
+    tail = DeviceBuffer(2 * (n - cut))  # the second block in its own (16-byte aligned) buffer,
+    tail.copy_from(dx, 2 * (n - cut), src_off=2 * cut)  # so it takes the int8 kernel too
+    g = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+    dz = DeviceBuffer.empty(n_out, np.complex64)
+    m1 = g.process_dev(dx.ptr, cut, dz.ptr, n_out)
+    m2 = g.process_dev(tail.ptr, n - cut, dz.ptr + 8 * m1, n_out - m1)
+    g.sync()
+    assert m1 + m2 == n_out
+    for m in range(0, n_out, 1 << 24):
+        c = min(1 << 24, n_out - m)
+        assert np.array_equal(dz.download(c, offset_bytes=8 * m), dy.download(c, offset_bytes=8 * m))
