@@ -162,12 +162,14 @@ def test_cu8_int8_tap_count_boundaries(sdr, oracle, K):
 
 
 @pytest.mark.parametrize("D,K", [(1, 1), (1, 64), (1, 177), (1, 178), (1, 255), (1, 257),
-                                 (2, 1), (2, 161), (2, 162), (2, 255), (2, 257)])
+                                 (2, 1), (2, 161), (2, 162), (2, 255), (2, 257),
+                                 (8, 1), (8, 129), (8, 130), (8, 255), (8, 257)])
 def test_cu8_int8_no_decimation(sdr, oracle, D, K):
-    """D = 1 and 2 u8 blocks on the int8 kernel (4 / D 256-output column sets per 1024-sample
-    tile, linear LDS): chunk-count boundaries (K = 177 / 178 at D = 1, 161 / 162 at D = 2),
-    ragged blocks (every decimation phase), a partial last tile, then a 3-channel bank whose
-    leading dimension keeps the 16-byte alignment."""
+    """D = 1, 2 and 8 u8 blocks on the int8 kernel (D = 1 / 2: 4 / D 256-output column sets per
+    1024-sample tile, linear LDS; D = 8: 2048-sample tiles, swizzled LDS): chunk-count
+    boundaries (K = 177 / 178 at D = 1, 161 / 162 at D = 2, 129 / 130 at D = 8), ragged blocks
+    (every decimation phase), a partial last tile, then a 3-channel bank whose leading
+    dimension keeps the 16-byte alignment."""
     from sdrgpu import _lib
     rng = np.random.default_rng(2000 + K + 7 * D)
     taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)

@@ -24,15 +24,15 @@ for K, n, cuts in ((255, 1 << 21, (0, 777, 300001, 1 << 21)), (97, 200003, (0, 2
     err = float(np.max(np.abs(y - ref)) / np.sqrt(np.mean(np.abs(ref) ** 2)))
     worst = max(worst, err)
     print(f"K {K} n {n} blocks {len(cuts) - 1}: max err / rms {err:.2e}")
-for K, n in ((255, 1 << 20), (61, 100003)):  # D = 1
+for K, n, D in ((255, 1 << 20, 1), (61, 100003, 1), (255, 1 << 20, 8), (255, 1 << 20, 2)):
     taps = ss.firwin(K, 0.2).astype(np.float32)
     raw = rng.integers(0, 256, size=2 * n, dtype=np.uint8)
-    ref = oracle.Fir(taps, 1, sample_kind=1).process(oracle.u8_to_c64(raw))
-    f = sdrgpu.filter.Fir(taps, decim=1, sample_kind=_lib.CU8).design(2.4e6)
+    ref = oracle.Fir(taps, D, sample_kind=1).process(oracle.u8_to_c64(raw))
+    f = sdrgpu.filter.Fir(taps, decim=D, sample_kind=_lib.CU8).design(2.4e6)
     y = np.concatenate([f.process(raw[:2 * 4097]), f.process(raw[2 * 4097:])])
     err = float(np.max(np.abs(y - ref)) / np.sqrt(np.mean(np.abs(ref) ** 2)))
     worst = max(worst, err)
-    print(f"D 1 K {K} n {n}: max err / rms {err:.2e}")
+    print(f"D {D} K {K} n {n}: max err / rms {err:.2e}")
 nch, nb = 5, 40000
 taps = ss.firwin(255, 0.2).astype(np.float32)
 x = rng.integers(0, 256, size=(nch, 2 * nb), dtype=np.uint8)

@@ -11,8 +11,8 @@ Phases (one JSON line each, per-launch ms in "ms"):
   long     300 further back-to-back launches
   idle     1 s host sleep (GPU idle), then 60 launches
 --kind: c64 = configs[1] (the headline), u8 = configs[1] fed from rtl_tcp u8 (bench_configs
-c2u8), bank = configs[4]'s 8192-channel D = 1 bank (bench.py's channel-sharded leg), u8d1 =
-2^26 rtl_tcp u8 samples through the 255-tap FIR without decimation.
+c2u8), bank = configs[4]'s 8192-channel D = 1 bank (bench.py's channel-sharded leg), u8dN =
+2^26 rtl_tcp u8 samples through the 255-tap FIR at decimation N (1, 2, 8).
 --clk: the library is tools/experiments/fir_ablate.sh's `clk` variant, which writes per
 workgroup (100 MHz ticks, shader-clock ticks) over the launch 4 KiB before its output
 pointer; each launch gets its own output offset so the records survive, and every phase
@@ -38,7 +38,7 @@ GUARD = 1024  # c64 elements (8 KiB) of output offset per launch under --clk
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1"])
+    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1", "u8d2", "u8d8"])
     ap.add_argument("--clk", action="store_true")
     ap.add_argument("--long", type=int, default=300)
     args = ap.parse_args()
@@ -62,14 +62,15 @@ def main():
 
         def launch(i):
             f.process_dev(x.ptr, n, n, y.ptr + 8 * guard * (i + 1), n)
-    elif args.kind == "u8d1":  # the u8 stream without Decimate: 2 B in + 8 B out per sample
+    elif args.kind.startswith("u8d"):  # u8 stream, decimation 1 / 2 / 8: 2 B in + 8/D B out per sample
         n = 1 << 26
-        f = sdrgpu.filter.Fir(taps, decim=1, sample_kind=_lib.CU8).design(2.4e6)
+        dec = int(args.kind[3:])
+        f = sdrgpu.filter.Fir(taps, decim=dec, sample_kind=_lib.CU8).design(2.4e6)
         pat = np.random.default_rng(21).integers(0, 256, size=2 * (1 << 22), dtype=np.uint8)
         x = DeviceBuffer.empty(2 * n, np.uint8)
         for off in range(0, 2 * n, pat.size):
             x.upload(pat[:min(pat.size, 2 * n - off)], offset_bytes=off)
-        out_n = n
+        out_n = n // dec
         y = DeviceBuffer.empty(out_n + guard * (nlaunch + 1), np.complex64)
 
         def launch(i):

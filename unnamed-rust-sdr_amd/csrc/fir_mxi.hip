@@ -25,6 +25,8 @@
 // registers) and columns v = the tile's 16 blocks (B = samples: B[p][v] = window[64 v + p]);
 // K = 320 window samples = 5 chunks of 64 (H = 256 history samples).
 //
+// D = 8: tiles of 2048 new samples (one column set), K = 6 chunks (K + 127 <= 384; 4 for
+// K <= 129), the 16-byte units XOR-swizzled within 256-byte lines (win_addr<8>).
 // D = 1 (the same stream without Decimate) and D = 2: rows are 16 outputs D samples apart,
 // columns blocks 16 D samples apart, K = 5 chunks cover K + 15 D + D - 1 <= 320; a tile is
 // 4 / D 256-output column sets over one staged window of H + 1024 samples (so the raw-tile
@@ -68,7 +70,7 @@ struct GeoI {
     static constexpr int WINB = 2 * WL;           // bytes per window buffer (I, Q planes)
     static constexpr int WAVE = 2 * WINB;         // bytes per wave (two buffers)
     static constexpr int HL = 64 - H / 8;         // first lane holding history (8 samples/lane)
-    static_assert(TI % 512 == 0 && H <= 512 && NG + 1 <= CS * NC, "geometry");
+    static_assert(TI % 512 == 0 && H <= 512 && CS * NC >= 2, "geometry");
     static_assert(D != 4 || OFF == 0, "geometry");
 };
 
@@ -122,10 +124,13 @@ __device__ __forceinline__ u32x4 fetch8(const unsigned short* in, const float2* 
 }
 
 // window sample b -> byte offset inside a plane: D = 4 swizzles 16-byte units within 64-byte
-// rows; at D = 1 and 2 (blocks 16 / 32 samples apart) the linear layout is already conflict free
+// rows; D = 8 (blocks 128 samples apart) XORs the 16-byte unit within its 256-byte line with
+// 2 (line & 3); at D = 1 and 2 (blocks 16 / 32 samples apart) the linear layout is already
+// conflict free
 template <int D>
 __device__ __forceinline__ int win_addr(int b) {
-    if constexpr (D != 4) return b;
+    if constexpr (D == 1 || D == 2) return b;
+    if constexpr (D == 8) return (b & ~255) | ((((b >> 4) & 15) ^ (2 * ((b >> 8) & 3))) << 4) | (b & 15);
     return 64 * (b >> 6) + 16 * (((b >> 4) & 3) ^ ((b >> 7) & 3)) + (b & 15);
 }
 
@@ -194,13 +199,20 @@ void fir_mxi_kernel(MxiParams p) {
         if constexpr (D == 4) {
             const int r = v + c;
             rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
+        } else if constexpr (D == 8) {
+            rb[c] = base + win_addr<8>(G::OFF + 128 * v + 64 * c + 16 * g);
         } else {
             rb[c] = base + G::OFF + 16 * D * v + 64 * c + 16 * g;
         }
     }
-    // staging addresses: lane l stages new samples 8 l + 512 k (k < NG: the row swizzle is the
-    // same for every k, so group k sits 512 k bytes on) and, if l >= HL, history samples 8 (l - HL)
+    // staging addresses: lane l stages new samples 8 l + 512 k (k < NG; at D = 1, 2 and 4 the
+    // swizzle is the same for every k, so group k sits 512 k bytes on, but not at D = 8) and,
+    // if l >= HL, history samples 8 (l - HL)
     const int wa0 = base + win_addr<D>(H + 8 * lane);
+    auto wa = [&](int k) __attribute__((always_inline)) {
+        if constexpr (D == 8) return base + win_addr<8>(H + 512 * k + 8 * lane);
+        return wa0 + 512 * k;
+    };
     const int wh = base + win_addr<D>(8 * (lane >= HL ? lane - HL : 0));
 
     // ---- the wave's tile stream (fir_mxh.hip's cursors, per-workgroup blocked units) ----
@@ -260,7 +272,7 @@ void fir_mxi_kernel(MxiParams p) {
         load_tile(nx, cm);
         if (lane >= HL) put8<WL>(smem, wh, hr);
 #pragma unroll
-        for (int k = 0; k < NG; ++k) put8<WL>(smem, wa0 + 512 * k, nx[k]);
+        for (int k = 0; k < NG; ++k) put8<WL>(smem, wa(k), nx[k]);
         st = cm;
         adv(st);
         if (st.ok && st.t == 0) load_hist(hr, st);
@@ -310,9 +322,9 @@ void fir_mxi_kernel(MxiParams p) {
                     if (ld_run) load_hist(hr, ld);
                 }
 #pragma unroll
-                for (int k = 0; k < NG; ++k) {
-                    if (k + 1 != i) continue;
-                    put8<WL>(smem, WN + wa0 + 512 * k, nx[k]);
+                for (int k = 0; k < NG; ++k) {  // group k at iteration k + 1 (the last takes the rest)
+                    if ((k + 1 < CS * NC ? k + 1 : CS * NC - 1) != i) continue;
+                    put8<WL>(smem, WN + wa(k), nx[k]);
                     nx[k] = __builtin_nontemporal_load(src2 + 64 * k + lane);
                 }
                 if (c == NC - 1) {  // column set j complete: scale and store its 256 outputs
@@ -374,6 +386,7 @@ void fir_mxi_kernel(MxiParams p) {
 
 int mxi_nc(int K, int D) {
     const int need = (K + 16 * D - 1 + 63) / 64;  // 64 NC >= K + 15 D + D - 1
+    if (D == 8) return need <= 4 ? 4 : (need <= 6 ? 6 : 0);
     return need <= 3 ? 3 : (need <= 5 ? 5 : 0);
 }
 
@@ -381,7 +394,7 @@ int mxi_nc(int K, int D) {
 
 int fir_mxi_supported(const FirParams& fp, int tap_scale_exp) {
     if (fp.sample_kind != SDRGPU_CU8 || fp.tap_kind != SDRGPU_F32) return 0;
-    if (!(fp.D == 4 || fp.D == 2 || fp.D == 1) || fp.K < 1 || fp.K > 257) return 0;
+    if (!(fp.D == 8 || fp.D == 4 || fp.D == 2 || fp.D == 1) || fp.K < 1 || fp.K > 257) return 0;
     if (mxi_nc(fp.K, fp.D) == 0 || fp.i0 < 0 || fp.i0 >= fp.D) return 0;
     // taps as 23-bit integers: 2^S and the output scale 2^-(S + 7) stay normal floats
     if (tap_scale_exp + 14 > 126 || tap_scale_exp + 7 < -126) return 0;
@@ -416,7 +429,7 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    const int cs = D == 4 ? kCs : (D == 2 ? kCs2 : kCs1);
+    const int cs = D >= 4 ? kCs : (D == 2 ? kCs2 : kCs1);
     p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     p.seg_tiles = std::max(1L, std::min<long>(std::max(1, kRunTiles / cs), p.tpc));
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
@@ -425,7 +438,9 @@ int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
 #define SDRGPU_MXI_GO(NCC, CSS, DD)                                                            \
     hipLaunchKernelGGL((fir_mxi_kernel<NCC, CSS, DD>), dim3(blocks), dim3(kBlock),             \
                        (size_t)kWaves * (GeoI<NCC, CSS, DD>::WAVE), s, p)
-    if (D == 4 && NC == 5) SDRGPU_MXI_GO(5, kCs, 4);
+    if (D == 8 && NC == 6) SDRGPU_MXI_GO(6, kCs, 8);
+    else if (D == 8) SDRGPU_MXI_GO(4, kCs, 8);
+    else if (D == 4 && NC == 5) SDRGPU_MXI_GO(5, kCs, 4);
     else if (D == 4) SDRGPU_MXI_GO(3, kCs, 4);
     else if (D == 2 && NC == 5) SDRGPU_MXI_GO(5, kCs2, 2);
     else if (D == 2) SDRGPU_MXI_GO(3, kCs2, 2);
