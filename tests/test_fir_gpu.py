@@ -376,3 +376,26 @@ def test_fir_mx_intra_window_dynamic_range(sdr, oracle, weak):
         mx, _ = rms_rel_err(y[w0:w0 + 64], ref[w0:w0 + 64])
         worst = max(worst, mx)
     assert worst <= 1e-5, f"worst 64-output window max/rms {worst:.3e} (weak {weak})"
+
+
+@pytest.mark.parametrize("K", [1, 129, 130, 255, 257])
+def test_fir_mx_decim2_fp16_tiles(sdr, oracle, K):
+    """c64 decimate-by-2 on the fp16 x 2 MFMA tiles (fir_mxh.hip at D = 2: 64-byte LDS rows with
+    a row swizzle, two 256-output column sets per 1024-sample tile): chunk-count boundary
+    K = 129 / 130, ragged blocks (both decimation phases, a partial last tile, carried history),
+    then a 3-channel bank."""
+    rng = np.random.default_rng(500 + K)
+    taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+    n = 6 * 1024 + 555
+    x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+    ref = oracle.Fir(taps, 2, sample_kind=1).process(x)
+    f = sdr.filter.Fir(taps, decim=2, sample_kind=1).design(2.4e6)
+    cuts = [0, 3, 1030, 2049, 4100, n]
+    y = np.concatenate([f.process(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    from sdrgpu import _lib
+    assert f.last_algorithm() == _lib.FIR_MATRIX
+    assert_parity(y, ref, what=f"K {K}")
+    xb = (rng.standard_normal((3, 5000)) + 1j * rng.standard_normal((3, 5000))).astype(np.complex64)
+    yb = sdr.filter.FirBank(taps, 3, sample_kind=1, decim=2).process(xb)
+    for c in range(3):
+        assert_parity(yb[c], oracle.Fir(taps, 2, sample_kind=1).process(xb[c]), what=f"bank K {K} ch {c}")

@@ -38,7 +38,7 @@ GUARD = 1024  # c64 elements (8 KiB) of output offset per launch under --clk
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1", "u8d2", "u8d8"])
+    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1", "u8d2", "u8d8", "c64d2"])
     ap.add_argument("--clk", action="store_true")
     ap.add_argument("--long", type=int, default=300)
     args = ap.parse_args()
@@ -62,6 +62,19 @@ def main():
 
         def launch(i):
             f.process_dev(x.ptr, n, n, y.ptr + 8 * guard * (i + 1), n)
+    elif args.kind == "c64d2":  # 2^26 c64 samples, decimation 2 (8 B in + 4 B out per sample)
+        n = 1 << 26
+        dec = 2
+        f = sdrgpu.filter.Fir(taps, decim=2, sample_kind=_lib.C64).design(2.4e6)
+        pat = bench.synth_iq_pattern(1 << 22, seed=1000)
+        x = DeviceBuffer.empty(n, np.complex64)
+        for off in range(0, n, pat.size):
+            x.upload(pat[:min(pat.size, n - off)], offset_bytes=8 * off)
+        out_n = n // 2
+        y = DeviceBuffer.empty(out_n + guard * (nlaunch + 1), np.complex64)
+
+        def launch(i):
+            f.process_dev(x.ptr, n, y.ptr + 8 * guard * (i + 1), out_n)
     elif args.kind.startswith("u8d"):  # u8 stream, decimation 1 / 2 / 8: 2 B in + 8/D B out per sample
         n = 1 << 26
         dec = int(args.kind[3:])

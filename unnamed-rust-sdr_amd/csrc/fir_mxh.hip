@@ -46,6 +46,8 @@ constexpr int kBlock = 64 * kWaves;
 // D = 1 tiles: three 256-output column sets share one staged window (2.48 vs 2.62 ms with one
 // set at configs[4]; profiles/r02_fir_d1_cs.txt), and 6 groups keep one raw tile in flight
 constexpr int kCs1 = 3;
+// D = 2 tiles: two 256-output column sets over one 1024-sample window (the D = 4 raw pipeline)
+constexpr int kCs2 = 2;
 // D = 4 runs.  c64 samples: runs of 2 tiles dealt grid-strided, so at any moment the whole
 // chip streams one contiguous window (2048 waves x 16 KiB): 0.441 ms, against 0.460 for the
 // same runs in per-workgroup ranges, 0.486-0.488 for per-workgroup runs of 8 (round 3 s3), and
@@ -70,7 +72,7 @@ struct GeoH {
     static constexpr int WAVE = 2 * WINB;          // bytes per wave
     static constexpr int NG = TI / 128;            // 128-sample groups per tile
     static constexpr int NH = H / 128;             // history groups
-    static_assert(HR > 0 && (D == 1 || (D == 4 && OFF == 0)), "geometry");
+    static_assert(HR > 0 && (D == 1 || ((D == 4 || D == 2) && OFF == 0)), "geometry");
     static_assert(kWaves * WAVE <= 160 * 1024, "LDS");
 };
 
@@ -272,12 +274,20 @@ void fir_mxh_kernel(MxhParams p) {
         if constexpr (D == 4) {
             const int r = sv + (c >> 1);
             rb[c] = base + 128 * r + 16 * ((4 * (c & 1) + g) ^ ((r >> 1) & 7));
+        } else if constexpr (D == 2) {
+            // 64-byte rows (32 samples), row r = v + c, 16-byte unit g ^ ((r >> 1) & 3): every
+            // 16-lane group of a fragment read hits distinct banks (fir_mxi.hip's D = 4 layout)
+            const int r = v + c;
+            rb[c] = base + 64 * r + 16 * (g ^ ((r >> 1) & 3));
         } else {
             rb[c] = base + 2 * (G::OFF + 16 * sv + 32 * c + 8 * g);
         }
     }
-    const int wb0 = D == 4 ? base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7)
-                           : base + 4 * lane;
+    // D = 2: sample s of a 128-sample group at 64 (s >> 5) + 16 (((s >> 3) & 3) ^ ((s >> 6) & 3))
+    // + 2 (s & 7); group k adds 256 k and flips unit bit 1 when k is odd
+    const int wb0 = D == 4   ? base + 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7)
+                    : D == 2 ? base + 64 * (lane >> 4) + 4 * (lane & 3) + 16 * (((lane >> 2) & 3) ^ (lane >> 5))
+                             : base + 4 * lane;
 
     // ---- the wave's tile stream ----
     // Units (runs of seg_tiles tiles of one channel) are dealt to waves either in per-
@@ -378,10 +388,12 @@ void fir_mxh_kernel(MxhParams p) {
     // byte offset of the sample pair (2 lane, 2 lane + 1) of history group k / new group k
     auto hist_addr = [&](int k) {
         if constexpr (D == 4) return (wb0 ^ (16 * (k & 7))) + 256 * k;
+        else if constexpr (D == 2) return (wb0 ^ (32 * (k & 1))) + 256 * k;
         else return wb0 + 256 * k;
     };
     auto new_addr = [&](int k) {
         if constexpr (D == 4) return (wb0 ^ (16 * ((H / 128 + k) & 7))) + 128 * (H / 64 + 2 * k);
+        else if constexpr (D == 2) return (wb0 ^ (32 * ((H / 128 + k) & 1))) + 2 * H + 256 * k;
         else return wb0 + 2 * H + 256 * k;
     };
     // next history = the last NH groups of (history ++ this tile's groups)
@@ -572,6 +584,10 @@ int mxh_nch(int K, int D) {
         const int need = (K + 15 + 31) / 32;  // 32 NCH >= K + 15
         return need <= 5 ? 5 : (need <= 9 ? 9 : 0);
     }
+    if (D == 2) {
+        const int need = (K + 31 + 31) / 32;  // 32 NCH >= K + 15*2 + 1
+        return need <= 5 ? 5 : (need <= 9 ? 9 : 0);
+    }
     return 0;
 }
 
@@ -588,7 +604,7 @@ int fir_mxh_shape_ok(int sample_kind, int tap_kind, int K, int D) {
 int fir_mxh_supported(const FirParams& fp) {
     const bool u8 = fp.sample_kind == SDRGPU_CU8;
     if ((!u8 && fp.sample_kind != SDRGPU_C64) || fp.tap_kind != SDRGPU_F32) return 0;
-    if (!(fp.D == 4 || (fp.D == 1 && !u8))) return 0;
+    if (!(fp.D == 4 || ((fp.D == 1 || fp.D == 2) && !u8))) return 0;
     if (fp.K < 1 || mxh_nch(fp.K, fp.D) == 0) return 0;
     if (fp.i0 < 0 || fp.i0 >= fp.D) return 0;
     // 16-byte (c64) / 4-byte (u8) loads of sample pairs: channel bases stay aligned
@@ -624,13 +640,13 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                     ? 1
                     : 0;
     const long nch = fp.nch;
-    const int cs = D == 1 ? kCs1 : 1;
+    const int cs = D == 1 ? kCs1 : (D == 2 ? kCs2 : 1);
     p.tpc = ceil_div(std::max(0L, fp.n_out), 256L * cs);
     const long W = (long)kWaves * cus;
     // D = 4: runs of kRunTiles tiles (c64: grid-strided; u8: per-CU blocks, round 2: 0.516-0.525
     // vs 0.556-0.559 ms with one long range per wave, profiles/r02_fir_runs.txt).  D = 1 banks
     // keep whole-channel units grid-strided (runs measured no faster there).
-    const int run = D == 4 ? (u8 ? kRunTilesU8 : kRunTiles) : 0;
+    const int run = D == 4 ? (u8 ? kRunTilesU8 : kRunTiles) : (D == 2 ? kRunTiles : 0);
     long spc = nch >= W ? 1 : ceil_div(W, nch);
     spc = std::max(1L, std::min(spc, p.tpc));
     p.seg_tiles = std::max(1L, ceil_div(p.tpc, spc));
@@ -655,12 +671,21 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
         SDRGPU_LAUNCH_CHECK();                                                                 \
         return SDRGPU_OK;                                                                      \
     }
+#define SDRGPU_MXH_CASE2(CC)                                                                   \
+    if (D == 2 && NCH == CC) {                                                                 \
+        SDRGPU_MXH_GO(CC, false, 2, kCs2);                                                     \
+        SDRGPU_LAUNCH_CHECK();                                                                 \
+        return SDRGPU_OK;                                                                      \
+    }
     SDRGPU_MXH_CASE(10)
     SDRGPU_MXH_CASE(6)
     SDRGPU_MXH_CASE1(9)
     SDRGPU_MXH_CASE1(5)
+    SDRGPU_MXH_CASE2(9)
+    SDRGPU_MXH_CASE2(5)
 #undef SDRGPU_MXH_CASE
 #undef SDRGPU_MXH_CASE1
+#undef SDRGPU_MXH_CASE2
 #undef SDRGPU_MXH_GO
     return SDRGPU_ERR_UNSUPPORTED;
 }
