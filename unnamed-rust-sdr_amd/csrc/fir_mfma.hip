@@ -357,8 +357,9 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
         fp.K != st->K)
         return SDRGPU_ERR_UNSUPPORTED;
-    // D = 4 and D = 1: the LDS-staged fp16 two-way split at two waves per SIMD (fir_mxh.hip);
-    // D = 2 / 8: the register-fed exact bf16 three-way split below
+    // D = 4, 2 and 1: the LDS-staged fp16 two-way split at two waves per SIMD (fir_mxh.hip);
+    // D = 8 (and D = 2 blocks the fp16 kernel does not take): the register-fed exact bf16
+    // three-way split below
     if (fir_mxh_supported(fp))
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
     if (st->NCH == 0) return SDRGPU_ERR_UNSUPPORTED;  // shape only the fp16 kernel covers
