@@ -165,14 +165,24 @@ def cpu_baseline(taps, seconds):
 KERNEL_SOURCES = ("unnamed-rust-sdr_amd/csrc/fir_mxh.hip", "unnamed-rust-sdr_amd/csrc/fir_kernels.hpp")
 
 
+def code_tokens(text):
+    """C/C++ source with comments removed and whitespace runs collapsed: what the compiler
+    sees, so a comment or layout edit does not change the hash below."""
+    import re
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    return " ".join(text.split())
+
+
 def kernel_source_sha16(root=ROOT):
-    """sha256[:16] over the headline kernel's source files: ties a committed PMC traffic
-    figure to the kernel build it was measured on (tools/pmc_to_json.py records it)."""
+    """sha256[:16] over the headline kernel's source files (comments and layout stripped,
+    code_tokens): ties a committed PMC traffic figure to the kernel code it was measured on
+    (tools/pmc_to_json.py records it)."""
     import hashlib
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
-        with open(os.path.join(root, rel), "rb") as f:
-            h.update(f.read())
+        with open(os.path.join(root, rel)) as f:
+            h.update(code_tokens(f.read()).encode())
     return h.hexdigest()[:16]
 
 

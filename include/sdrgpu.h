@@ -70,6 +70,19 @@ enum sdrgpu_fir_algo {
                                      aligned input.  AUTO picks it for those shapes. */
 };
 
+/* Which kernel ran the most recent block (sdrgpu_fir_last_kernel; test / bench introspection,
+ * no reference counterpart).  The CU8 bit is set when rtl_tcp u8 input was first converted to
+ * c64 by its own launch (shapes and alignments the fused u8 kernels do not take). */
+enum sdrgpu_fir_kernel {
+    SDRGPU_FIR_KERNEL_NONE = 0,
+    SDRGPU_FIR_KERNEL_FP16 = 1,          /* fir_mxh: LDS-staged per-tile scaled fp16 x2 MFMA */
+    SDRGPU_FIR_KERNEL_INT8 = 2,          /* fir_mxi: rtl_tcp u8 on the int8 MFMAs (16-B aligned) */
+    SDRGPU_FIR_KERNEL_BF16X3 = 3,        /* fir_mfma: register-fed exact bf16 x3 MFMA */
+    SDRGPU_FIR_KERNEL_OVERLAP_SAVE = 4,
+    SDRGPU_FIR_KERNEL_DIRECT = 5,
+    SDRGPU_FIR_KERNEL_CU8_CONVERTED = 16  /* flag */
+};
+
 const char* sdrgpu_strerror(int code);   /* resample::Error Display, src/resample.rs:209-269 */
 int sdrgpu_abi_version(void);
 int sdrgpu_device_count(int* count);
@@ -143,6 +156,7 @@ int sdrgpu_fir_sync(sdrgpu_fir* h);
  * non-empty block; SDRGPU_FIR_AUTO before the first one.  Introspection for tests and
  * benches (which kernel family a shape actually took); no reference counterpart. */
 int sdrgpu_fir_last_algorithm(const sdrgpu_fir* h, int* algo);
+int sdrgpu_fir_last_kernel(const sdrgpu_fir* h, int* kernel);  /* sdrgpu_fir_kernel */
 int sdrgpu_fir_reset(sdrgpu_fir* h);                           /* FilterDesign::design -> fresh state */
 int sdrgpu_fir_clone(const sdrgpu_fir* h, sdrgpu_fir** out);   /* #[derive(Clone)] Fir, fir.rs:6 */
 void sdrgpu_fir_destroy(sdrgpu_fir* h);
@@ -164,6 +178,7 @@ int sdrgpu_firbank_process_dev(sdrgpu_firbank* h, const void* d_in, size_t ld_in
                                size_t n_in, void* d_out, size_t ld_out, size_t* n_out);
 int sdrgpu_firbank_sync(sdrgpu_firbank* h);
 int sdrgpu_firbank_last_algorithm(const sdrgpu_firbank* h, int* algo);
+int sdrgpu_firbank_last_kernel(const sdrgpu_firbank* h, int* kernel);
 int sdrgpu_firbank_reset(sdrgpu_firbank* h);
 int sdrgpu_firbank_clone(const sdrgpu_firbank* h, sdrgpu_firbank** out);
 void sdrgpu_firbank_destroy(sdrgpu_firbank* h);

@@ -119,15 +119,51 @@ def test_cu8_int8_and_fp16_kernels(sdr, oracle):
             assert f.process_dev(dx.ptr + off, n, dy.ptr, n_out) == n_out
             f.sync()
             assert f.last_algorithm() == _lib.FIR_MATRIX
+            want = _lib.FIR_KERNEL_INT8 if off == 0 else _lib.FIR_KERNEL_FP16
+            assert f.last_kernel() == want, (K, off, f.last_kernel())
             assert_parity(dy.download(), ref, what=f"K{K} offset {off}")
     taps = (rng.standard_normal(255) / 16).astype(np.float32)
     for nb in (8192 + 24, 8192 + 26):  # leading dim % 8 == 0 (int8) / != 0 (fp16)
         nch = 4
         x = rng.integers(0, 256, size=(nch, 2 * nb), dtype=np.uint8)
-        y = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=4).process(x)
+        bank = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=4)
+        y = bank.process(x)
+        want = _lib.FIR_KERNEL_INT8 if nb % 8 == 0 else _lib.FIR_KERNEL_FP16
+        assert bank.last_kernel() == want, (nb, bank.last_kernel())
         for c in range(nch):
             ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(x[c]))
             assert_parity(y[c], ref, what=f"bank nb {nb} ch {c}")
+
+
+def test_cu8_mixed_kernel_stream(sdr, oracle):
+    """One u8 stream whose blocks alternate between 16-byte aligned device buffers (int8
+    kernel), 4-byte aligned ones (fp16 kernel) and 2-byte aligned ones (converted to c64 first,
+    then the fp16 kernel): the kernel of each block follows the buffer, the history carries
+    across the switches, and the whole output stays within the tolerance.  The bits of an
+    output depend on which kernel produced it (a documented non-guarantee)."""
+    from sdrgpu import _lib
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(404)
+    taps = (rng.standard_normal(255) / 16).astype(np.float32)
+    n = 9 * 4096 + 1234
+    raw = u8_stream(rng, n)
+    ref = oracle.Fir(taps, 4, sample_kind=1).process(oracle.u8_to_c64(raw))
+    f = sdr.filter.Fir(taps, decim=4, sample_kind=_lib.CU8).design(2.4e6)
+    cuts = [0, 4096, 8192 + 3, 12289, 20000, 24576, 30001, n]
+    offs = [0, 4, 2, 0, 4, 0, 2]
+    want = {0: _lib.FIR_KERNEL_INT8, 4: _lib.FIR_KERNEL_FP16,
+            2: _lib.FIR_KERNEL_FP16 | _lib.FIR_KERNEL_CU8_CONVERTED}
+    dx = DeviceBuffer(2 * n + 32)
+    outs = []
+    for (a, b), off in zip(zip(cuts[:-1], cuts[1:]), offs):
+        dx.upload(raw[2 * a:2 * b], offset_bytes=off)
+        m = f.output_len(b - a)
+        dy = DeviceBuffer.empty(max(m, 1), np.complex64)
+        assert f.process_dev(dx.ptr + off, b - a, dy.ptr, m) == m
+        f.sync()
+        assert f.last_kernel() == want[off], (a, off, f.last_kernel())
+        outs.append(dy.download()[:m])
+    assert_parity(np.concatenate(outs), ref, what="mixed-kernel stream")
 
 
 @pytest.mark.parametrize("scale", [1e-25, 3e-8, 1.0, 5e6, 1e25])
@@ -180,10 +216,13 @@ def test_cu8_int8_no_decimation(sdr, oracle, D, K):
     cuts = [0, 5, 1029, 2048, 4100, n]
     y = np.concatenate([f.process(raw[2 * a:2 * b]) for a, b in zip(cuts[:-1], cuts[1:])])
     assert f.last_algorithm() == _lib.FIR_MATRIX
+    assert f.last_kernel() == _lib.FIR_KERNEL_INT8, f.last_kernel()
     assert_parity(y, ref, what=f"K {K}")
     nch, nb = 3, 4096 + 8
     x = rng.integers(0, 256, size=(nch, 2 * nb), dtype=np.uint8)
-    yb = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=D).process(x)
+    bank = sdr.filter.FirBank(taps, nch, sample_kind=_lib.CU8, decim=D)
+    yb = bank.process(x)
+    assert bank.last_kernel() == _lib.FIR_KERNEL_INT8, bank.last_kernel()
     for c in range(nch):
         assert_parity(yb[c], oracle.Fir(taps, D, sample_kind=1).process(oracle.u8_to_c64(x[c])),
                       what=f"bank K {K} ch {c}")

@@ -1,0 +1,131 @@
+"""Instrument copies of pll.hip and the ONE FIR build for the configs[3] chain probe
+(round 5, VERDICT r4 "Next 1").  Never part of the product library.
+
+  python tools/diag/pll_probe_patch.py PLL_SRC_OUT BANK_SRC_IN BANK_SRC_OUT
+
+PLL copy (pll_split_kernel only; the LDS footprint and the ring stores are unchanged):
+  * wave 0 writes every (c.re, phasedif) it puts into the ring to a global shadow [ch][s];
+  * wave 1 writes the (c.re, phasedif) it read back from the ring to [ch][s];
+  * lane 0 of each wave records HW_ID, LDS_ALLOC, XCC_ID and s_memrealtime at start / end.
+Bank copy (D = 1 instantiations): lane 0 of wave 0 records the same registers per workgroup.
+Both expose an extern "C" fetch of their device arrays (sdrgpu_probe_fetch / _bank_fetch).
+"""
+import sys
+
+pll_out, bank_in, bank_out = sys.argv[1:4]
+
+PROBE_SAMPLES = 1024  # per channel
+s = open("unnamed-rust-sdr_amd/csrc/pll.hip").read()
+
+glob = f"""
+namespace sdrgpu_probe {{
+constexpr int kS = {PROBE_SAMPLES};
+__device__ float2 shadow[1024 * kS];
+__device__ float2 readb[1024 * kS];
+__device__ unsigned long long hw[64][2][4];
+__device__ __forceinline__ void rec_hw(int slot) {{
+    if ((threadIdx.x & 63) == 0) {{
+        const int w = threadIdx.x >> 6;
+        unsigned long long* r = hw[blockIdx.x & 63][w];
+        if (slot == 0) {{
+            r[0] = __builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID (32 bits)
+            r[1] = __builtin_amdgcn_s_getreg(0xF806);   // HW_REG_LDS_ALLOC
+            r[2] = __builtin_amdgcn_s_getreg(0xF814);   // HW_REG_XCC_ID
+            r[3] = __builtin_amdgcn_s_memrealtime();
+        }} else {{
+            r[2] |= (unsigned long long)__builtin_amdgcn_s_memrealtime() << 8;  // end time (low 56 bits)
+        }}
+    }}
+}}
+}}  // namespace sdrgpu_probe
+"""
+anchor = "namespace sdrgpu {\n\nnamespace {"
+assert anchor in s
+s = s.replace(anchor, glob + "\n" + anchor, 1)
+
+old = "    PllChannelState s = state[ch];\n    const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;\n    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;\n    auto cvt = [](unsigned w) -> float2 {\n        return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);\n    };\n    float* __restrict__ y = out + ch * ld_out;\n    uint8_t* __restrict__ lk = locked + ch * ld_out;\n    const Bq L"
+assert s.count(old) == 1, s.count(old)
+s = s.replace(old, old.replace("    PllChannelState s = state[ch];", "    sdrgpu_probe::rec_hw(0);\n    PllChannelState s = state[ch];"), 1)
+
+old = "                ring[c & 1][k][lane] = chain(cur[k]);\n"
+assert s.count(old) == 1
+s = s.replace(old, """                {
+                    const float2 cp = chain(cur[k]);
+                    ring[c & 1][k][lane] = cp;
+                    const long si = c * kChunk + k;
+                    if (si < sdrgpu_probe::kS && ch < 1024) sdrgpu_probe::shadow[ch * sdrgpu_probe::kS + si] = cp;
+                }
+""", 1)
+
+old = """            for (int k = 0; k < kChunk; ++k)
+                filters(ring[c & 1][k][lane], MODE == 1 ? ring1[MODE == 1 ? (c & 1) : 0][k][lane] : float4{},
+                        ov[k], lv[k]);
+"""
+assert s.count(old) == 1
+s = s.replace(old, """            for (int k = 0; k < kChunk; ++k) {
+                const float2 rd = ring[c & 1][k][lane];
+                const long si = c * kChunk + k;
+                if (si < sdrgpu_probe::kS && ch < 1024) sdrgpu_probe::readb[ch * sdrgpu_probe::kS + si] = rd;
+                filters(rd, MODE == 1 ? ring1[MODE == 1 ? (c & 1) : 0][k][lane] : float4{}, ov[k], lv[k]);
+            }
+""", 1)
+
+old = "    __syncthreads();\n    if (wv != 0) return;\n    // wave 0: the filter states back"
+assert s.count(old) == 1
+s = s.replace(old, "    __syncthreads();\n    sdrgpu_probe::rec_hw(1);\n    if (wv != 0) return;\n    // wave 0: the filter states back", 1)
+
+s += """
+extern "C" int sdrgpu_probe_fetch(int which, void* dst, size_t bytes) {
+    const void* sym = which == 0 ? (const void*)&sdrgpu_probe::shadow
+                    : which == 1 ? (const void*)&sdrgpu_probe::readb
+                                 : (const void*)&sdrgpu_probe::hw;
+    if (dst) return (int)hipMemcpyFromSymbol(dst, sym, bytes, 0, hipMemcpyDeviceToHost);
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, sym) != hipSuccess) return -1;
+    if (hipMemset(p, 0xff, bytes) != hipSuccess) return -1;  // reset to NaN / all-ones
+    return (int)hipDeviceSynchronize();
+}
+"""
+open(pll_out, "w").write(s)
+
+b = open(bank_in).read()
+bglob = """
+namespace sdrgpu_probe_bank {
+__device__ unsigned long long hw[1024][4];
+}
+"""
+anchor = "namespace sdrgpu {\n\nnamespace {"
+assert anchor in b
+b = b.replace(anchor, bglob + "\n" + anchor, 1)
+old = "    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);\n"
+assert b.count(old) == 1
+b = b.replace(old, old + """    if constexpr (D == 1) {
+        if (threadIdx.x == 0 && blockIdx.x < 1024) {
+            unsigned long long* r = sdrgpu_probe_bank::hw[blockIdx.x];
+            r[0] = __builtin_amdgcn_s_getreg(0xF804);
+            r[1] = __builtin_amdgcn_s_getreg(0xF806);
+            r[2] = __builtin_amdgcn_s_getreg(0xF814);
+            r[3] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+""", 1)
+old = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
+assert b.count(old) == 1
+b = b.replace(old, """    if constexpr (D == 1) {
+        if (threadIdx.x == 0 && blockIdx.x < 1024)
+            sdrgpu_probe_bank::hw[blockIdx.x][2] |= (unsigned long long)__builtin_amdgcn_s_memrealtime() << 8;
+    }
+""" + old, 1)
+b += """
+extern "C" int sdrgpu_probe_bank_fetch(void* dst, size_t bytes) {
+    if (dst) return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sdrgpu_probe_bank::hw), bytes, 0, hipMemcpyDeviceToHost);
+    void* p = nullptr;
+    hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(sdrgpu_probe_bank::hw));
+    if (e != hipSuccess) return 1000 + (int)e;
+    e = hipMemset(p, 0, bytes);
+    if (e != hipSuccess) return 2000 + (int)e;
+    return (int)hipDeviceSynchronize();
+}
+"""
+open(bank_out, "w").write(b)
+print("patched", pll_out, bank_out)

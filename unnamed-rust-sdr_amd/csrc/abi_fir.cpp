@@ -19,7 +19,7 @@ void* fir_os_prepare(int device, int sample_kind, int tap_kind, const void* taps
 void fir_os_release(void* os_state);
 int fir_mx_supported(int sample_kind, int tap_kind, int K, int D);
 void* fir_mx_prepare(int device, const float* taps, int K, int D, int* status);
-int fir_mx_launch(const FirParams& p, void* state, hipStream_t s);
+int fir_mx_launch(const FirParams& p, void* state, hipStream_t s, int* kernel);
 void fir_mx_release(void* state);
 int cu8_to_c64_launch(const void* in, long ld_in, long n, long nch, void* out, hipStream_t s);
 }  // namespace sdrgpu
@@ -32,6 +32,7 @@ struct FirCore {
     size_t nch = 1;
     int algo = SDRGPU_FIR_AUTO;
     int last_algo = SDRGPU_FIR_AUTO;       // path that ran the most recent block
+    int last_kernel = SDRGPU_FIR_KERNEL_NONE;  // and its kernel (sdrgpu_fir_kernel)
     std::vector<unsigned char> taps_host;  // original taps (for clone / OS prep)
     int tpp = 0;
     void* d_taps_pm = nullptr;
@@ -189,11 +190,12 @@ struct FirCore {
         p.force_naive = 0;
         int st = SDRGPU_ERR_UNSUPPORTED;
         int ran = SDRGPU_FIR_MATRIX;
+        int kern = SDRGPU_FIR_KERNEL_NONE, conv = 0;
         if (want_mx()) {
             if (!mx_state && mx_status == SDRGPU_OK)
                 mx_state = fir_mx_prepare(device, reinterpret_cast<const float*>(taps_host.data()),
                                           K, D, &mx_status);
-            if (mx_state) st = fir_mx_launch(p, mx_state, stream.cur);  // CU8: fused ingest
+            if (mx_state) st = fir_mx_launch(p, mx_state, stream.cur, &kern);  // CU8: fused ingest
             else if (mx_status != SDRGPU_ERR_UNSUPPORTED) return mx_status;
             // an unaligned buffer (UNSUPPORTED) falls through to the other paths
             if (st != SDRGPU_OK && st != SDRGPU_ERR_UNSUPPORTED) return st;
@@ -208,9 +210,10 @@ struct FirCore {
             p.sample_kind = SDRGPU_C64;
             p.in = stage_conv.ptr;
             p.ld_in = (long)n_in;
+            conv = SDRGPU_FIR_KERNEL_CU8_CONVERTED;
             st = SDRGPU_ERR_UNSUPPORTED;
             if (want_mx() && mx_state) {
-                st = fir_mx_launch(p, mx_state, stream.cur);
+                st = fir_mx_launch(p, mx_state, stream.cur, &kern);
                 if (st != SDRGPU_OK && st != SDRGPU_ERR_UNSUPPORTED) return st;
             }
         }
@@ -220,14 +223,17 @@ struct FirCore {
                 os_state = fir_os_prepare(device, csk, tk, taps_host.data(), K, D, stream.cur,
                                           &os_status);
             if (os_state) st = fir_os_launch(p, os_state, stream.cur);
+            kern = SDRGPU_FIR_KERNEL_OVERLAP_SAVE;
             if (st != SDRGPU_OK && algo == SDRGPU_FIR_OVERLAP_SAVE) return st;
         }
         if (st != SDRGPU_OK) {
             ran = SDRGPU_FIR_DIRECT;
             st = fir_direct_launch(p, stream.cur);
+            kern = SDRGPU_FIR_KERNEL_DIRECT;
         }
         if (st) return st;
         last_algo = ran;
+        last_kernel = kern | conv;
         if (K > 1) cur ^= 1;
         seen += n_in;
         return SDRGPU_OK;
@@ -412,6 +418,12 @@ int sdrgpu_fir_last_algorithm(const sdrgpu_fir* h, int* algo) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_fir_last_kernel(const sdrgpu_fir* h, int* kernel) {
+    if (!h || !kernel) return SDRGPU_ERR_INVALID;
+    *kernel = h->core.last_kernel;
+    return SDRGPU_OK;
+}
+
 int sdrgpu_fir_reset(sdrgpu_fir* h) {
     if (!h) return SDRGPU_ERR_INVALID;
     return h->core.reset_state();
@@ -514,6 +526,12 @@ int sdrgpu_firbank_sync(sdrgpu_firbank* h) {
 int sdrgpu_firbank_last_algorithm(const sdrgpu_firbank* h, int* algo) {
     if (!h || !algo) return SDRGPU_ERR_INVALID;
     *algo = h->core.last_algo;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_firbank_last_kernel(const sdrgpu_firbank* h, int* kernel) {
+    if (!h || !kernel) return SDRGPU_ERR_INVALID;
+    *kernel = h->core.last_kernel;
     return SDRGPU_OK;
 }
 

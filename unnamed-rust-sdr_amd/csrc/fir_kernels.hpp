@@ -50,7 +50,7 @@ int fir_os_supported(int sample_kind, int tap_kind, int K, int D);
 // of zeroed device memory (target of the clamped prefetches at a stream's end).
 size_t fir_mxh_dummy_bytes();
 int fir_mxh_supported(const FirParams& p);
-int fir_mxh_shape_ok(int sample_kind, int tap_kind, int K, int D);  // D in {1, 4}
+int fir_mxh_shape_ok(int sample_kind, int tap_kind, int K, int D);  // c64: D in {1, 2, 4}; u8: D = 4
 int fir_mxh_launch(const FirParams& p, const float* d_taps, int tap_scale_exp,
                    const void* d_dummy, int cus, hipStream_t s);
 

@@ -344,14 +344,19 @@ void fir_mx_release(void* state) {
     delete st;
 }
 
-int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
+int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s, int* kernel) {
+    int dummy_kernel = 0;
+    int& kern = kernel ? *kernel : dummy_kernel;
     auto* st = static_cast<MxState*>(state);
     if (st && fp.sample_kind == SDRGPU_CU8) {  // rtl_tcp u8 ingest fused into the FIR load
         if (fp.D != st->D || fp.K != st->K) return SDRGPU_ERR_UNSUPPORTED;
         // the int8-MFMA kernel (16-byte aligned channels), else the fp16 one (4-byte aligned)
-        if (st->taps_finite && fir_mxi_supported(fp, st->tap_scale_exp))
+        if (st->taps_finite && fir_mxi_supported(fp, st->tap_scale_exp)) {
+            kern = SDRGPU_FIR_KERNEL_INT8;
             return fir_mxi_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
+        }
         if (!fir_mxh_supported(fp)) return SDRGPU_ERR_UNSUPPORTED;
+        kern = SDRGPU_FIR_KERNEL_FP16;
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
     }
     if (!st || fp.sample_kind != SDRGPU_C64 || fp.tap_kind != SDRGPU_F32 || fp.D != st->D ||
@@ -360,8 +365,10 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     // D = 4, 2 and 1: the LDS-staged fp16 two-way split at two waves per SIMD (fir_mxh.hip);
     // D = 8 (and D = 2 blocks the fp16 kernel does not take): the register-fed exact bf16
     // three-way split below
-    if (fir_mxh_supported(fp))
+    if (fir_mxh_supported(fp)) {
+        kern = SDRGPU_FIR_KERNEL_FP16;
         return fir_mxh_launch(fp, st->d_taps, st->tap_scale_exp, st->d_dummy, st->cus, s);
+    }
     if (st->NCH == 0) return SDRGPU_ERR_UNSUPPORTED;  // shape only the fp16 kernel covers
     // 16-byte loads of sample pairs: channel bases must stay 16-byte aligned
     if ((reinterpret_cast<uintptr_t>(fp.in) & 15) != 0 || (fp.nch > 1 && (fp.ld_in & 1)))
@@ -395,6 +402,7 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s) {
     dim3 grid((unsigned)std::max(1L, ceil_div(waves, kMxBlock / 64)));
 #define SDRGPU_MX_CASE(DD, CC)                                                                   \
     if (D == DD && NCH == CC) {                                                                  \
+        kern = SDRGPU_FIR_KERNEL_BF16X3;                                                         \
         hipLaunchKernelGGL((fir_mx_kernel<DD, CC>), grid, dim3(kMxBlock), 0, s, p);                \
         SDRGPU_LAUNCH_CHECK();                                                                   \
         return SDRGPU_OK;                                                                        \

@@ -79,7 +79,7 @@ struct MxiParams {
     long ld_in, n_in;         // per channel, in samples (2 bytes)
     const float2* hist;
     float2* hist_next;
-    const unsigned char* dummy;  // >= 2 KiB readable: target of clamped prefetches
+    const unsigned char* dummy;  // >= 2 TI bytes readable (one raw tile): target of clamped prefetches
     long n_out;
     int K;
     int delta;  // D - 1 - i0
@@ -406,9 +406,12 @@ int fir_mxi_supported(const FirParams& fp, int tap_scale_exp) {
 
 int fir_mxi_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
                    const void* d_dummy, int cus, hipStream_t s) {
-    if (!fir_mxi_supported(fp, tap_scale_exp) || !d_dummy || fir_mxh_dummy_bytes() < 2048)
-        return SDRGPU_ERR_UNSUPPORTED;
+    if (!fir_mxi_supported(fp, tap_scale_exp) || !d_dummy) return SDRGPU_ERR_UNSUPPORTED;
     const int D = fp.D;
+    // a clamped prefetch reads one whole raw tile (NG groups x 64 lanes x 16 B = 2 TI bytes)
+    // from the dummy buffer: 4 KiB at D = 8
+    const long tile_bytes = 2L * 256 * D * (D >= 4 ? kCs : (D == 2 ? kCs2 : kCs1));
+    if ((long)fir_mxh_dummy_bytes() < tile_bytes) return SDRGPU_ERR_UNSUPPORTED;
     const int NC = mxi_nc(fp.K, D);
     MxiParams p;
     p.in = static_cast<const unsigned char*>(fp.in);

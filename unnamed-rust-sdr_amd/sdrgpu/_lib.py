@@ -30,6 +30,15 @@ FIR_DIRECT = 1
 FIR_OVERLAP_SAVE = 2
 FIR_MATRIX = 3
 
+# sdrgpu_fir_kernel: which kernel ran the last block (last_kernel())
+FIR_KERNEL_NONE = 0
+FIR_KERNEL_FP16 = 1
+FIR_KERNEL_INT8 = 2
+FIR_KERNEL_BF16X3 = 3
+FIR_KERNEL_OVERLAP_SAVE = 4
+FIR_KERNEL_DIRECT = 5
+FIR_KERNEL_CU8_CONVERTED = 16
+
 FFT_OUT_COMPLEX = 0
 FFT_OUT_DB = 1
 
@@ -103,6 +112,7 @@ SIGNATURES = [
     ("sdrgpu_fir_process_async", c_int, [_H, c_void_p, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_fir_sync", c_int, [_H]),
     ("sdrgpu_fir_last_algorithm", c_int, [_H, POINTER(c_int)]),
+    ("sdrgpu_fir_last_kernel", c_int, [_H, POINTER(c_int)]),
     ("sdrgpu_fir_reset", c_int, [_H]),
     ("sdrgpu_fir_clone", c_int, [_H, _PH]),
     ("sdrgpu_fir_destroy", None, [_H]),
@@ -119,6 +129,7 @@ SIGNATURES = [
      [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, _PS]),
     ("sdrgpu_firbank_sync", c_int, [_H]),
     ("sdrgpu_firbank_last_algorithm", c_int, [_H, POINTER(c_int)]),
+    ("sdrgpu_firbank_last_kernel", c_int, [_H, POINTER(c_int)]),
     ("sdrgpu_firbank_reset", c_int, [_H]),
     ("sdrgpu_firbank_clone", c_int, [_H, _PH]),
     ("sdrgpu_firbank_destroy", None, [_H]),

@@ -189,6 +189,13 @@ class FirFilter:
         check(lib().sdrgpu_fir_last_algorithm(self._h, ctypes.byref(a)), "last_algorithm")
         return a.value
 
+    def last_kernel(self) -> int:
+        """FIR_KERNEL_*: the kernel of the last block (| FIR_KERNEL_CU8_CONVERTED when u8
+        input was converted to c64 by its own launch first)."""
+        a = ctypes.c_int()
+        check(lib().sdrgpu_fir_last_kernel(self._h, ctypes.byref(a)), "last_kernel")
+        return a.value
+
 
 class FirBank:
     """nch independent Fir<C,A> (fir.rs:6-32) sharing taps; channel-major blocks."""
@@ -279,6 +286,11 @@ class FirBank:
     def last_algorithm(self) -> int:
         a = ctypes.c_int()
         check(lib().sdrgpu_firbank_last_algorithm(self._h, ctypes.byref(a)), "last_algorithm")
+        return a.value
+
+    def last_kernel(self) -> int:
+        a = ctypes.c_int()
+        check(lib().sdrgpu_firbank_last_kernel(self._h, ctypes.byref(a)), "last_kernel")
         return a.value
 
 
