@@ -185,3 +185,52 @@ def test_c4_matched_filter_into_pll_chain(sdr, oracle, nch, n, cut):
     assert np.array_equal(lk, ref_lk), f"lock mask differs in {np.sum(lk != ref_lk)} samples"
     assert np.array_equal(out, ref_out), f"{np.sum(out != ref_out)} PLL outputs differ"
     assert lk.any() and out[lk.astype(bool)].std() > 0  # the chain locks and demodulates
+
+
+@pytest.mark.parametrize("K", [127, 255])
+def test_pll_beside_concurrent_mfma_bank(sdr, oracle, K):
+    """The main.rs PLL (src/main.rs:41-46; src/filter/pll.rs:70-85) over 1024 channels while
+    matched-filter bank launches (D = 1 MFMA kernel, src/filter/fir.rs:23-32 per channel) stream
+    over other buffers on another stream for the PLL's whole run.  K = 127 takes the bank
+    instantiation that leaves room for another wave on each of its SIMDs (176 VGPRs per wave).
+    Round 5 measured the PLL chain's packed-f32 mixer going wrong in lanes 48-63 when MFMA bank
+    waves shared its SIMD; the PLL kernels now claim their SIMD whole.  Outputs
+    and lock flags array_equal to the oracle PLL; the bank's last block within tolerance."""
+    from sdrgpu.device import DeviceBuffer
+    import scipy.signal as ss
+    from test_pll_gpu import RATE, fm_channels, main_rs_design, oracle_params
+    rng = np.random.default_rng(500 + K)
+    nch, n = 1024, 4096
+    x = fm_channels(rng, nch, n)
+    pll = main_rs_design(sdr).design(RATE, nch=nch)
+    dx = DeviceBuffer.from_numpy(x)
+    do = DeviceBuffer.empty(nch * n, np.float32)
+    dl = DeviceBuffer.empty(nch * n, np.uint8)
+    taps = ss.firwin(K, 0.2).astype(np.float32)
+    nb_ch, nb = 1024, 16384
+    xb = cplx(rng, (nb_ch, nb)) * np.float32(0.3)
+    b = bank(sdr, taps, nb_ch)
+    dxb = DeviceBuffer.from_numpy(xb)
+    dyb = DeviceBuffer.empty(nb_ch * nb, np.complex64)
+    b.sync()
+    pll.process_dev(dx.ptr, n, n, do.ptr, dl.ptr, n)      # ~1.2 ms of PLL on its stream ...
+    reps = 24                                              # ... beside ~24 bank launches
+    for _ in range(reps):
+        assert b.process_dev(dxb.ptr, nb, nb, dyb.ptr, nb) == nb
+    b.sync()
+    pll.sync()
+    out = do.download(dtype=np.float32).reshape(nch, n)
+    lk = dl.download(dtype=np.uint8).reshape(nch, n)
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)
+    bad = (out != ref_out) | (lk != ref_lk)
+    if bad.any():
+        chs = np.unique(np.nonzero(bad)[0])
+        raise AssertionError(f"PLL beside the bank: {int(bad.sum())} samples wrong in {chs.size} "
+                             f"channels (lanes {sorted(set((chs % 64).tolist()))[:16]})")
+    assert lk.any() and out[lk.astype(bool)].std() > 0
+    # the bank's last launch: the stream of reps identical blocks, checked on a few channels
+    y = dyb.download().reshape(nb_ch, nb)
+    for c in (0, 517, nb_ch - 1):
+        stream = np.tile(xb[c], reps)
+        ref = oracle.Fir(taps, 1, sample_kind=1).process(stream)[-nb:]
+        assert_parity(y[c], ref, what=f"bank ch {c}")

@@ -1,17 +1,31 @@
 #!/bin/bash
-# Build the configs[3] chain probe library (tools/diag/probe_build/lib_probe.so): the product
-# objects with fir_mxh.o replaced by the instrumented ONE build and pll.o by the instrumented
-# PLL (tools/diag/pll_probe_patch.py).  Diagnostic only; never the product library.
+# Build the configs[3] chain probe libraries (tools/diag/probe_build/lib_hw_<name>.so): the
+# product objects with fir_mxh.o replaced by an instrumented bank (start-only HW_ID records) and
+# pll.o by an instrumented PLL (tools/diag/pll_probe_patch.py).  Diagnostic only.
 set -e
 cd "$(dirname "$0")/../.."
 make -C unnamed-rust-sdr_amd -s
 O=tools/diag/probe_build
 mkdir -p $O
-python3 tools/diag/pll_probe_patch.py $O/pll_probe.hip ${BANK_SRC:-tools/experiments/fir_mxh_one.hip} $O/fir_mxh_probe.hip
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip"
-/opt/rocm/bin/hipcc $F -ffp-contract=off -c $O/pll_probe.hip -o $O/pll_probe.o &
-/opt/rocm/bin/hipcc $F -c $O/fir_mxh_probe.hip -o $O/fir_mxh_probe.o &
-wait
+python3 tools/diag/pll_vgpr_variant.py $O/pll_scalar96.hip 0 5 scalar
+# name bank_src pll_src opts
+VARS="one_split:tools/experiments/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:-
+one_shadow:tools/experiments/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:--shadow
+one_scalar96:tools/experiments/fir_mxh_one.hip:$O/pll_scalar96.hip:-
+prod_split:unnamed-rust-sdr_amd/csrc/fir_mxh.hip:unnamed-rust-sdr_amd/csrc/pll.hip:-"
 OBJS=$(ls unnamed-rust-sdr_amd/build/*.o | grep -v -e '/fir_mxh.o' -e '/pll.o')
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $O/lib_probe.so $OBJS $O/pll_probe.o $O/fir_mxh_probe.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-echo built $O/lib_probe.so
+for v in $VARS; do
+  IFS=: read name bsrc psrc opt <<< "$v"
+  python3 tools/diag/pll_probe_patch.py $O/hw_pll_$name.hip $bsrc $O/hw_fir_$name.hip --pll-src=$psrc $opt
+  ( /opt/rocm/bin/hipcc $F -ffp-contract=off -c $O/hw_pll_$name.hip -o $O/hw_pll_$name.o -Rpass-analysis=kernel-resource-usage 2> $O/hw_pll_$name.res &&
+    /opt/rocm/bin/hipcc $F -c $O/hw_fir_$name.hip -o $O/hw_fir_$name.o -Rpass-analysis=kernel-resource-usage 2> $O/hw_fir_$name.res &&
+    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $O/lib_hw_$name.so $OBJS $O/hw_pll_$name.o $O/hw_fir_$name.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib ) &
+done
+wait
+for v in $VARS; do
+  name=${v%%:*}
+  echo "$name: bank D=1 NCH=9 $(grep -A2 'ILi9ELb0ELi1ELi3E' $O/hw_fir_$name.res | grep -m1 -o 'VGPRs: [0-9]*')," \
+       "pll main.rs split $(grep -A2 'pll_split_kernelILb0ELi0ELi1ELi0ELi0E' $O/hw_pll_$name.res | grep -m1 -o 'VGPRs: [0-9]*')," \
+       "scalar $(grep -A2 'pll_kernelILb0ELi0ELi1ELi0ELi0ELb1E' $O/hw_pll_$name.res | grep -m1 -o 'VGPRs: [0-9]*')"
+done

@@ -13,15 +13,21 @@ Both expose an extern "C" fetch of their device arrays (sdrgpu_probe_fetch / _ba
 import sys
 
 pll_out, bank_in, bank_out = sys.argv[1:4]
+opts = set(sys.argv[4:])  # --shadow: ring shadow / read-back; --end: end-time stamps (raise VGPR use)
+pll_src = "unnamed-rust-sdr_amd/csrc/pll.hip"
+for o in opts:
+    if o.startswith("--pll-src="):
+        pll_src = o.split("=", 1)[1]
 
 PROBE_SAMPLES = 1024  # per channel
-s = open("unnamed-rust-sdr_amd/csrc/pll.hip").read()
+s = open(pll_src).read()
 
 glob = f"""
 namespace sdrgpu_probe {{
 constexpr int kS = {PROBE_SAMPLES};
-__device__ float2 shadow[1024 * kS];
+__device__ float4 shadow[1024 * kS];  // (v.re, v.im after the step, c.re, c.im) of wave 0
 __device__ float2 readb[1024 * kS];
+__device__ float4 shadow2[1024 * kS];  // (nphase, v.re, v.im, 0) after the step
 __device__ unsigned long long hw[64][2][4];
 __device__ __forceinline__ void rec_hw(int slot) {{
     if ((threadIdx.x & 63) == 0) {{
@@ -46,14 +52,24 @@ s = s.replace(anchor, glob + "\n" + anchor, 1)
 old = "    PllChannelState s = state[ch];\n    const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;\n    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;\n    auto cvt = [](unsigned w) -> float2 {\n        return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);\n    };\n    float* __restrict__ y = out + ch * ld_out;\n    uint8_t* __restrict__ lk = locked + ch * ld_out;\n    const Bq L"
 assert s.count(old) == 1, s.count(old)
 s = s.replace(old, old.replace("    PllChannelState s = state[ch];", "    sdrgpu_probe::rec_hw(0);\n    PllChannelState s = state[ch];"), 1)
+# the split kernel's chain: keep c.im visible to the shadow store
+ks = s.index("void pll_split_kernel(")
+old = "        const float ci = v.x * cji + v.y * cjr;\n"
+i = s.index(old, ks)
+s = s[:i] + old + "        dbg_ci = ci;\n" + s[i + len(old):]
+old = "    auto chain = [&](float2 v) -> float2 {\n"
+i = s.index(old, ks)
+s = s[:i] + "    float dbg_ci = 0.f;\n" + s[i:]
 
 old = "                ring[c & 1][k][lane] = chain(cur[k]);\n"
 assert s.count(old) == 1
-s = s.replace(old, """                {
+if "--shadow" in opts:
+  s = s.replace(old, """                {
                     const float2 cp = chain(cur[k]);
                     ring[c & 1][k][lane] = cp;
                     const long si = c * kChunk + k;
-                    if (si < sdrgpu_probe::kS && ch < 1024) sdrgpu_probe::shadow[ch * sdrgpu_probe::kS + si] = cp;
+                    if (si < sdrgpu_probe::kS && ch < 1024)
+                        sdrgpu_probe::shadow[ch * sdrgpu_probe::kS + si] = make_float4(s.vr, s.vi, cp.x, dbg_ci);
                 }
 """, 1)
 
@@ -62,7 +78,8 @@ old = """            for (int k = 0; k < kChunk; ++k)
                         ov[k], lv[k]);
 """
 assert s.count(old) == 1
-s = s.replace(old, """            for (int k = 0; k < kChunk; ++k) {
+if "--shadow" in opts:
+  s = s.replace(old, """            for (int k = 0; k < kChunk; ++k) {
                 const float2 rd = ring[c & 1][k][lane];
                 const long si = c * kChunk + k;
                 if (si < sdrgpu_probe::kS && ch < 1024) sdrgpu_probe::readb[ch * sdrgpu_probe::kS + si] = rd;
@@ -72,12 +89,14 @@ s = s.replace(old, """            for (int k = 0; k < kChunk; ++k) {
 
 old = "    __syncthreads();\n    if (wv != 0) return;\n    // wave 0: the filter states back"
 assert s.count(old) == 1
-s = s.replace(old, "    __syncthreads();\n    sdrgpu_probe::rec_hw(1);\n    if (wv != 0) return;\n    // wave 0: the filter states back", 1)
+if "--end" in opts:
+  s = s.replace(old, "    __syncthreads();\n    sdrgpu_probe::rec_hw(1);\n    if (wv != 0) return;\n    // wave 0: the filter states back", 1)
 
 s += """
 extern "C" int sdrgpu_probe_fetch(int which, void* dst, size_t bytes) {
     const void* sym = which == 0 ? (const void*)&sdrgpu_probe::shadow
                     : which == 1 ? (const void*)&sdrgpu_probe::readb
+                    : which == 3 ? (const void*)&sdrgpu_probe::shadow2
                                  : (const void*)&sdrgpu_probe::hw;
     if (dst) return (int)hipMemcpyFromSymbol(dst, sym, bytes, 0, hipMemcpyDeviceToHost);
     void* p = nullptr;
@@ -86,6 +105,9 @@ extern "C" int sdrgpu_probe_fetch(int which, void* dst, size_t bytes) {
     return (int)hipDeviceSynchronize();
 }
 """
+old = "    const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;\n    if (ch >= p.nch) return;\n"
+assert s.count(old) == 1
+s = s.replace(old, "    sdrgpu_probe::rec_hw(0);\n" + old, 1)
 open(pll_out, "w").write(s)
 
 b = open(bank_in).read()
@@ -97,9 +119,11 @@ __device__ unsigned long long hw[1024][4];
 anchor = "namespace sdrgpu {\n\nnamespace {"
 assert anchor in b
 b = b.replace(anchor, bglob + "\n" + anchor, 1)
-old = "    if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);\n"
+old = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
 assert b.count(old) == 1
-b = b.replace(old, old + """    if constexpr (D == 1) {
+# bank placement recorded at the END of the main loop only (a record at the start keeps values
+# live through the loop and raised the bank's VGPR count 201 -> 233, which changes co-residency)
+b = b.replace(old, """    if constexpr (D == 1) {
         if (threadIdx.x == 0 && blockIdx.x < 1024) {
             unsigned long long* r = sdrgpu_probe_bank::hw[blockIdx.x];
             r[0] = __builtin_amdgcn_s_getreg(0xF804);
@@ -107,13 +131,6 @@ b = b.replace(old, old + """    if constexpr (D == 1) {
             r[2] = __builtin_amdgcn_s_getreg(0xF814);
             r[3] = __builtin_amdgcn_s_memrealtime();
         }
-    }
-""", 1)
-old = "    if (p.hist_next) {  // stream history carry, spread over the whole grid"
-assert b.count(old) == 1
-b = b.replace(old, """    if constexpr (D == 1) {
-        if (threadIdx.x == 0 && blockIdx.x < 1024)
-            sdrgpu_probe_bank::hw[blockIdx.x][2] |= (unsigned long long)__builtin_amdgcn_s_memrealtime() << 8;
     }
 """ + old, 1)
 b += """

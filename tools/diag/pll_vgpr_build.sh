@@ -11,10 +11,10 @@ F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iincl
 /opt/rocm/bin/hipcc $F -c tools/experiments/fir_mxh_one.hip -o $O/fir_one.o &
 cp unnamed-rust-sdr_amd/build/fir_mxh.o $O/fir_prod.o
 # name split_cap scalar_cap route
-VARS="orig:0:0:split scalar96:0:5:scalar split80:6:0:split scalar80:0:6:scalar"
+VARS="orig:0:0:split:- scalar96:0:5:scalar:- split80:6:0:split:- scalar80:0:6:scalar:- splitx:0:0:split:excl scalarx:0:0:scalar:excl"
 for v in $VARS; do
-  IFS=: read name sc kc route <<< "$v"
-  python3 tools/diag/pll_vgpr_variant.py $O/pll_$name.hip $sc $kc $route
+  IFS=: read name sc kc route ex <<< "$v"
+  python3 tools/diag/pll_vgpr_variant.py $O/pll_$name.hip $sc $kc $route $ex
   /opt/rocm/bin/hipcc $F -ffp-contract=off -c $O/pll_$name.hip -o $O/pll_$name.o &
 done
 wait

@@ -36,12 +36,19 @@ __device__ __forceinline__ float bq_step(const float* c, float x, float& x1, flo
     return out;
 }
 
+// A bit-exact recurrence built from packed-f32 VALU ops, like the PLL chain: each wave owns its
+// SIMD (512 VGPRs claimed), so no MFMA wave of a concurrently running kernel can share it (the
+// measured hazard is described at pll.hip's own_simd).  One channel per lane, so this costs
+// nothing below 64 Ki channels.
+__device__ __forceinline__ void own_simd() { asm volatile("" ::: "v255", "a255"); }
+
 template <bool CPLX>
 __global__ __launch_bounds__(kBqBlock) void biquad_kernel(long nch, float b0, float b1, float b2,
                                                           float na1, float na2, int ident,
                                                           const float* __restrict__ in, long ld_in,
                                                           long n, float* __restrict__ out,
                                                           long ld_out, BiquadState* __restrict__ st) {
+    own_simd();
     const long ch = (long)blockIdx.x * kBqBlock + threadIdx.x;
     if (ch >= nch) return;
     constexpr int W = CPLX ? 2 : 1;  // floats per sample

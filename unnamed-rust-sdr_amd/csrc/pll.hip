@@ -33,6 +33,18 @@ namespace {
 constexpr int kPllBlock = 64;   // one wave: 64 channels
 constexpr int kChunk = 8;       // samples per lane per pipeline stage
 
+// Every PLL wave owns its SIMD: the kernels claim the whole register file (v255 and a255 are
+// named, so each wave allocates 512 VGPRs and no other wave -- of any kernel -- can be resident
+// on that SIMD while it runs).  Measured reason (round 5, DESIGN 3.6, profiles/r05_chain_probe.txt):
+// with two waves of a D = 1 MFMA FIR bank on the same SIMD (a bank build at 201 VGPRs leaves
+// room for a 96-VGPR PLL wave), the chain wave's mixer c = x * conj(v) -- a v_pk_mul_f32 whose
+// result the next v_pk_add_f32 reads -- came out as c.re = x.re * v.re in lanes 48-63 at one
+// sample (the product y * v.im read as 0), and the chaotic loop then diverged; inputs, the
+// NCO value and the LDS hand-off were all right, and nothing in the ISA orders one wave's
+// VALU results against another wave's.  With the SIMD to itself the chain is bit-exact again,
+// at the same speed (a PLL wave alone on its SIMD is what it is sized for anyway).
+__device__ __forceinline__ void own_simd() { asm volatile("" ::: "v255", "a255"); }
+
 struct Bq {
     float b0, b1, b2, na1, na2;
 };
@@ -67,6 +79,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
                                                         long ld_in, long n, float* __restrict__ out,
                                                         uint8_t* __restrict__ locked, long ld_out,
                                                         PllChannelState* __restrict__ state) {
+    own_simd();
     const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
     if (ch >= p.nch) return;
     PllChannelState s = state[ch];
@@ -226,6 +239,7 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
     // output mode 1 (the stereo pilot) also needs the input's real part and the new NCO value
     __shared__ float4 ring1[MODE == 1 ? 2 : 1][kChunk][kPllBlock];
     __shared__ float fst[8][kPllBlock];  // the helper's filter states, handed back at the end
+    own_simd();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // lanes past the last channel run a copy of the last channel and store nothing (every
     // lane takes part in the per-chunk barriers)
