@@ -114,3 +114,60 @@ def test_mxh_d2_layout_reads_what_was_staged_conflict_free(NCH):
                     assert [written[p + e] for e in range(8)] == list(range(a, a + 16, 2))
                     addrs.append(a)
                 assert conflict_free_b128(addrs), (NCH, j, c, grp[:4])
+
+
+def mxh_layout(D, NCH, CS):
+    """fir_mxh.hip's GeoH + staging address functions (byte offsets in one plane of a wave's
+    ring, relative to the window start), as in the kernel."""
+    TO = 256 * CS
+    TI = TO * D
+    HR = 32 * NCH - 16 * D
+    H = (HR + 127) // 128 * 128
+
+    def wb0(lane):
+        if D == 4:
+            return 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7)
+        if D == 2:
+            return 64 * (lane >> 4) + 4 * (lane & 3) + 16 * (((lane >> 2) & 3) ^ (lane >> 5))
+        return 4 * lane
+
+    def hist_addr(k, lane):
+        if D == 4:
+            return (wb0(lane) ^ (16 * (k & 7))) + 256 * k
+        if D == 2:
+            return (wb0(lane) ^ (32 * (k & 1))) + 256 * k
+        return wb0(lane) + 256 * k
+
+    def new_addr(k, lane):
+        if D == 4:
+            return (wb0(lane) ^ (16 * ((H // 128 + k) & 7))) + 128 * (H // 64 + 2 * k)
+        if D == 2:
+            return (wb0(lane) ^ (32 * ((H // 128 + k) & 1))) + 2 * H + 256 * k
+        return wb0(lane) + 2 * H + 256 * k
+
+    return TI, H, hist_addr, new_addr
+
+
+@pytest.mark.parametrize("D,NCH,CS", [(4, 10, 1), (4, 6, 1), (2, 9, 2), (2, 5, 2), (1, 9, 3), (1, 5, 3), (1, 9, 4), (1, 5, 4)])
+def test_mxh_ring_odd_history_is_the_even_windows_tail(D, NCH, CS):
+    """fir_mxh.hip's LDS ring (R = H + 2 TI samples; even tiles' window at 0, odd tiles' at TI):
+    the bytes where an even window's staging puts its last H new samples are exactly where an
+    odd window's history staging (hist_addr, relative to the odd window) would put them, so an
+    odd tile that continues the run reads its history in place.  The even history [0, H) and
+    the odd window [TI, R) are disjoint, and the ring holds both windows."""
+    TI, H, hist_addr, new_addr = mxh_layout(D, NCH, CS)
+    NG, NH = TI // 128, H // 128
+    R = H + 2 * TI
+    WODD = 2 * TI                                    # bytes: TI samples x 2 B per plane
+    even = {}                                        # window sample -> byte (even window)
+    for k in range(NG):
+        for lane in range(64):
+            a = new_addr(k, lane)
+            even[H + 128 * k + 2 * lane] = a
+    for k in range(NH):                              # odd history sample s (odd-relative)
+        for lane in range(64):
+            s = 128 * k + 2 * lane
+            assert WODD + hist_addr(k, lane) == even[TI + s], (k, lane)
+    assert TI >= H
+    top = max(max(new_addr(k, l) for k in range(NG) for l in range(64)), 0) + 4
+    assert top <= 2 * (H + TI) and WODD + top <= 2 * R      # both windows inside the ring

@@ -22,10 +22,15 @@
 // 2^-24 of its largest term); samples more than 2^-24 below that maximum (or |x| < 2^-111)
 // fall into fp16 subnormals.  f32's exponent range is otherwise kept (any input scale).
 //
-// LDS per wave: two window buffers (tile t computes from one while tile t+1 is staged into
-// the other -- no aliasing, no ordering constraints), each 4 planes (hi/lo x re/im) of
-// H + 1024 bf16-sized samples: 2 x 4 x 1280 x 2 B = 20 KiB at NCH = 10, so 8 waves fill the
-// 160 KiB of a CU exactly.
+// LDS per wave: a ring of R = H + 2 TI samples in 4 planes (hi/lo x re/im, 2 B each).  Even
+// tiles of the wave's stream use window [0, H + TI), odd tiles [TI, R): an odd tile's history
+// (the H samples before it) is the tail of the even tile's window, already staged -- when the
+// odd tile continues the even tile's run and keeps its scale (sticky scale below), it is not
+// staged again.  Tile t computes from its window while tile t+1 is staged into the other; the
+// even window's last H samples overlap the odd window's history, so an even tile's last NH
+// groups (and an odd tile's history, when it has to be staged) are written after the MFMA
+// loop of the tile being computed.  4 x 2304 x 2 B = 18 KiB at NCH = 10 (was 20 KiB with
+// two separate window buffers).
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -43,9 +48,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;               // two waves per SIMD
 constexpr int kBlock = 64 * kWaves;
-// D = 1 tiles: three 256-output column sets share one staged window (2.48 vs 2.62 ms with one
-// set at configs[4]; profiles/r02_fir_d1_cs.txt), and 6 groups keep one raw tile in flight
-constexpr int kCs1 = 3;
+// D = 1 tiles: four 256-output column sets share one staged window (one set: 2.62 ms at
+// configs[4], three: 2.48, profiles/r02_fir_d1_cs.txt; four fit only in the LDS ring: 2.037
+// vs 2.079 ms for three in the driver window, profiles/r05_fir_ring_ab.txt); 8 groups keep
+// one raw tile in flight
+constexpr int kCs1 = 4;
 // D = 2 tiles: two 256-output column sets over one 1024-sample window (the D = 4 raw pipeline)
 constexpr int kCs2 = 2;
 // D = 4 runs.  c64 samples: runs of 2 tiles dealt grid-strided, so at any moment the whole
@@ -66,13 +73,16 @@ struct GeoH {
     static constexpr int HR = 32 * NCH - 16 * D;   // history samples a tile's windows need
     static constexpr int H = (HR + 127) / 128 * 128;  // staged history (128-sample groups)
     static constexpr int OFF = H - HR;             // window offset inside the buffer
-    static constexpr int WL = H + TI;              // window samples
-    static constexpr int PLB = 2 * WL;             // bytes per plane
-    static constexpr int WINB = 4 * PLB;           // bytes per window buffer
-    static constexpr int WAVE = 2 * WINB;          // bytes per wave
+    static constexpr int R = H + 2 * TI;           // ring samples per plane
+    static constexpr int PLB = 2 * R;              // bytes per plane
+    static constexpr int WODD = 2 * TI;            // byte offset of the odd tiles' window
+    static constexpr int WAVE = 4 * PLB;           // bytes per wave
     static constexpr int NG = TI / 128;            // 128-sample groups per tile
     static constexpr int NH = H / 128;             // history groups
     static_assert(HR > 0 && (D == 1 || ((D == 4 || D == 2) && OFF == 0)), "geometry");
+    // even history [0, H) must stay clear of the odd window [TI, R); the row swizzles of D = 4
+    // (period 16 rows of 64 samples) and D = 2 (8 rows of 32) repeat every TI samples
+    static_assert(TI >= H && (D == 1 || TI % 1024 == 0), "ring");
     static_assert(kWaves * WAVE <= 160 * 1024, "LDS");
 };
 
@@ -223,7 +233,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fir_mxh_kernel(MxhParams p) {
     using Raw = std::conditional_t<U8, unsigned, float4>;
     using G = GeoH<NCH, D, CS>;
-    constexpr int H = G::H, HR = G::HR, PLB = G::PLB, WINB = G::WINB, NH = G::NH, NG = G::NG;
+    constexpr int H = G::H, HR = G::HR, PLB = G::PLB, NH = G::NH, NG = G::NG;
     constexpr int TI = G::TI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -407,6 +417,7 @@ void fir_mxh_kernel(MxhParams p) {
 
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
+    static_assert(NG > NH, "an even window's last NH groups come from keep[]");
     Cur cm, st, ld;
     seek(cm, p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave);
     if (cm.ok) {
@@ -430,8 +441,9 @@ void fir_mxh_kernel(MxhParams p) {
         adv(ld);
 
         auto body = [&](auto tau_c) {
-            constexpr int TAU = decltype(tau_c)::value;
-            constexpr int WN = (1 - TAU) * WINB;  // staging buffer offset
+            constexpr int TAU = decltype(tau_c)::value;  // parity of tile k (computed)
+            constexpr int P = 1 - TAU;                   // parity of tile k+1 (staged)
+            constexpr int WN = P * G::WODD;              // staging window offset
             const bool fast2 = ld.ok && tile_fast(ld);
             const bool ld_run = ld.ok && ld.t == 0;  // tile k+2 opens a run: reload history
             // prefetch source: tile k+2, or the zeroed dummy buffer (scalar select)
@@ -439,7 +451,17 @@ void fir_mxh_kernel(MxhParams p) {
             const float2* src2 = fast2 ? p.in + ld.ch * p.ld_in + j2 : p.dummy;
             const unsigned* src2u = fast2 ? p.in_u8 + ld.ch * (p.ld_in / 2) + (j2 >> 1)
                                           : reinterpret_cast<const unsigned*>(p.dummy);
-            const int s_next = window_scale(nx, hr);
+            // Sticky scale: an odd tile that continues the run of the even tile before it finds
+            // its history already staged (the even window's tail) and keeps that tile's scale
+            // while its window max stays within [2^7, 2^16) at it (s_fresh - s_cur in [-1, 7]:
+            // no fp16 overflow; the lo parts' 2^-24 quantum stays below 2^-31 of the max).
+            // Otherwise (even tiles, run starts, scale changes) the window gets its own scale
+            // 2^s, s = 15 - exponent(max), and its history is staged.
+            const int s_fresh = window_scale(nx, hr);
+            const int dsc = s_fresh - s_cur;
+            const bool keep_scale = P == 1 && st.t > 0 && dsc >= -1 && dsc <= 7;
+            const int s_next = keep_scale ? s_cur : s_fresh;
+            const bool hist_late = P == 1 && !keep_scale;  // odd window: history after the loop
             const float scn = exp2i(s_next);
             constexpr int NK = NG < NH ? NG : NH;  // staged groups that become history
             Raw keep[NK];
@@ -452,7 +474,7 @@ void fir_mxh_kernel(MxhParams p) {
             u32x4 fb[2][4];
             // column set j of the tile reads 256 samples (D = 1) further into the window
             auto read_frags = [&](u32x4 (&f)[4], int c, int j) {
-                const int a = rb[c] + TAU * WINB + j * 2 * 256 * D;
+                const int a = rb[c] + TAU * G::WODD + j * 2 * 256 * D;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (!U8 || (q & 1) == 0)
@@ -482,15 +504,18 @@ void fir_mxh_kernel(MxhParams p) {
                     cr[j] = mfma(ah[c], f[0], cr[j]);
                     ci[j] = mfma(ah[c], f[2], ci[j]);
                 }
-                if (i == 0) {  // window k+1's history (old hr); then tile k+2's, if it opens a run
+                if (i == 0) {  // even window k+1's history (old hr); then tile k+2's, if it opens a run
+                    if (P == 0) {
 #pragma unroll
-                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
-                    if (ld_run) load_hist(hr, ld);
+                        for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
+                    }
+                    if (ld_run && !hist_late) load_hist(hr, ld);
                 }
 #pragma unroll
                 for (int k = 0; k < NG; ++k) {
                     if ((k < CS * NCH - 1 ? k : CS * NCH - 1) != i) continue;
-                    put(WN + new_addr(k), nx[k], scn);
+                    // an even window's last NH groups overlap the odd window being read: later
+                    if (P == 1 || k < NG - NH) put(WN + new_addr(k), nx[k], scn);
                     if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
                     if constexpr (U8) {
                         nx[k] = __builtin_nontemporal_load(src2u + 64 * k + lane);
@@ -499,6 +524,18 @@ void fir_mxh_kernel(MxhParams p) {
                             reinterpret_cast<const f32x4*>(src2 + 128 * k + 2 * lane));
                         nx[k] = make_float4(r[0], r[1], r[2], r[3]);
                     }
+                }
+            }
+            // after tile k's last fragment reads (same wave, LDS in order): the writes that land
+            // in tile k's window
+            if constexpr (P == 0) {
+#pragma unroll
+                for (int k = NG - NH; k < NG; ++k) put(WN + new_addr(k), keep[k - (NG - NH)], scn);
+            } else {
+                if (hist_late) {
+#pragma unroll
+                    for (int k = 0; k < NH; ++k) put(WN + hist_addr(k), hr[k], scn);
+                    if (ld_run) load_hist(hr, ld);
                 }
             }
             if (!ld_run) {  // history of tile k+2's window: roll in the staged tile's tail
