@@ -54,7 +54,7 @@ def test_pmc_traffic_tied_to_kernel_source(tmp_path):
 def test_committed_pmc_file_matches_the_shipped_kernel():
     """profiles/pmc_fir_c2.json is the figure bench.py reports as roofline.traffic: it must
     have been measured on the fir_mxh source in this tree (re-measure after a kernel change:
-    tools/gpu/r02_final.sh's FETCH / WRITE passes -> tools/pmc_to_json.py)."""
+    tools/gpu/final.sh's FETCH / WRITE passes -> tools/pmc_to_json.py)."""
     t, src = bench.pmc_traffic(os.path.join(ROOT, "profiles", "pmc_fir_c2.json"), 28, "auto")
     assert t is not None, src
     assert 1.0 <= t / (10 * (1 << 28)) <= 1.1

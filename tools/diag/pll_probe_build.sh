@@ -9,10 +9,11 @@ O=tools/diag/probe_build
 mkdir -p $O
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip"
 python3 tools/diag/pll_vgpr_variant.py $O/pll_scalar96.hip 0 5 scalar
+bash tools/experiments/one_source.sh $O/fir_mxh_one.hip
 # name bank_src pll_src opts
-VARS="one_split:tools/experiments/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:-
-one_shadow:tools/experiments/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:--shadow
-one_scalar96:tools/experiments/fir_mxh_one.hip:$O/pll_scalar96.hip:-
+VARS="one_split:$O/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:-
+one_shadow:$O/fir_mxh_one.hip:unnamed-rust-sdr_amd/csrc/pll.hip:--shadow
+one_scalar96:$O/fir_mxh_one.hip:$O/pll_scalar96.hip:-
 prod_split:unnamed-rust-sdr_amd/csrc/fir_mxh.hip:unnamed-rust-sdr_amd/csrc/pll.hip:-"
 OBJS=$(ls unnamed-rust-sdr_amd/build/*.o | grep -v -e '/fir_mxh.o' -e '/pll.o')
 for v in $VARS; do

@@ -8,7 +8,8 @@ make -C unnamed-rust-sdr_amd -s
 O=tools/diag/probe_build
 mkdir -p $O
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Iunnamed-rust-sdr_amd/csrc -Iinclude -x hip"
-/opt/rocm/bin/hipcc $F -c tools/experiments/fir_mxh_one.hip -o $O/fir_one.o &
+bash tools/experiments/one_source.sh $O/fir_mxh_one.hip
+/opt/rocm/bin/hipcc $F -c $O/fir_mxh_one.hip -o $O/fir_one.o &
 cp unnamed-rust-sdr_amd/build/fir_mxh.o $O/fir_prod.o
 # name split_cap scalar_cap route
 VARS="orig:0:0:split:- scalar96:0:5:scalar:- split80:6:0:split:- scalar80:0:6:scalar:- splitx:0:0:split:excl scalarx:0:0:scalar:excl"

@@ -253,9 +253,9 @@ s = s.replace(old, "    const bool one = false && !u8 && D == 4")
 open(p, 'w').write(s)
 PY
   elif [ $part = r3src ]; then  # the round-3 fir_mxh.hip (commit 76500ef), rebuilt (bisect)
-    cp tools/experiments/fir_mxh_r3.hip $src
-  elif [ $part = one ]; then  # round 4's ONE instantiation + factored body (tools/experiments/fir_mxh_one.hip): faster, but the configs[3] chain test mismatches beside it
-    cp tools/experiments/fir_mxh_one.hip $src
+    git show 76500ef:unnamed-rust-sdr_amd/csrc/fir_mxh.hip > $src
+  elif [ $part = one ]; then  # round 4's ONE instantiation + factored body (tools/experiments/one_source.sh): faster, but the configs[3] chain test mismatched beside it until the PLL waves owned their SIMD
+    bash tools/experiments/one_source.sh $src
   elif [ $part = canary ]; then  # D = 1 launches get 16 KiB more LDS (a CU then holds no other workgroup beside a bank workgroup), filled with a pattern and checked at the end (printf CANARY on a change)
     python3 - $src <<'PY'
 import sys

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build variants of the int8-MFMA u8 FIR kernel (fir_mxi.hip) into tools/experiments/abl/
 # (never into the product library).  Run one with:
-#   python tools/experiments/run_with_lib.py tools/experiments/abl/lib_mxi_<v>.so tools/gpu/r04_series.py --kind u8
+#   python tools/experiments/run_with_lib.py tools/experiments/abl/lib_mxi_<v>.so tools/gpu/series.py --kind u8
 #   gs2 / gs4 : units of 2 / 4 tiles dealt grid-strided (the c64 headline's dealing)
 #   b4 / b16  : per-workgroup runs of 4 / 16 tiles (product: 8)
 #   w16       : two 8-wave workgroups per CU (4 waves per SIMD, <= 128 VGPRs)

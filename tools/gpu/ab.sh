@@ -2,7 +2,7 @@
 # A/B of the product library against a baseline build (BASE=path to a .so, default
 # tools/diag/probe_build/lib_base.so: the previous build, copied there before the change;
 # git-ignored, travels with the snapshot): REPS alternations of the per-launch series
-# (tools/gpu/r04_series.py --kind K for K in KINDS), summarised as driver-window (launches
+# (tools/gpu/series.py --kind K for K in KINDS), summarised as driver-window (launches
 # 6-25: what `bench.py --steps 20 --warmup 5` times) and steady-state (last 200) means.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -14,9 +14,9 @@ for rep in $(seq 1 ${REPS:-3}); do
   for v in base new; do
     for kind in ${KINDS:-c64}; do
       if [ $v = base ]; then
-        timeout -k 10 120 python -u tools/experiments/run_with_lib.py $BASE tools/gpu/r04_series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
+        timeout -k 10 120 python -u tools/experiments/run_with_lib.py $BASE tools/gpu/series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
       else
-        timeout -k 10 120 python -u tools/gpu/r04_series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
+        timeout -k 10 120 python -u tools/gpu/series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
       fi
     done
   done

@@ -1,10 +1,12 @@
 #!/bin/bash
-# Round-4 evidence pass: GPU tests, smoke, the driver's bench command (+ a rocprofv3 kernel
-# trace / stats of that same command), FETCH / WRITE PMC of the headline launch, all
-# bench_configs lines, 2-rank rehearsals.  Outputs under gpurun_out/$FINAL_DIR/.
+# Evidence pass for a tree (outputs under gpurun_out/$OUT): the driver's GPU suite, smoke, the
+# driver's bench command plus a rocprofv3 kernel trace / stats of that same command, FETCH and
+# WRITE PMC passes of the headline launch (-> pmc_fir_c2.json via tools/pmc_to_json.py),
+# every bench_configs line, and the 2-rank rehearsals (one GPU shared).  SKIP_TESTS / SKIP_HEAD
+# / SKIP_CONFIGS skip a part; U8PROF=1 adds the rtl_tcp u8 launch's trace and PMC.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${FINAL_DIR:-r04_final}
+O=$R/gpurun_out/${OUT:-final}
 mkdir -p $O
 cd $R
 if [ -z "$SKIP_TESTS" ]; then
@@ -32,7 +34,7 @@ cut -c1-500 $O/c5_2rank.jsonl
 timeout -k 10 300 python -u bench.py --gpus 2 --no-cpu-baseline --steps 10 --warmup 2 > $O/bench_2rank.jsonl 2> $O/bench_2rank.err || { tail -20 $O/bench_2rank.err; exit 9; }
 cut -c1-300 $O/bench_2rank.jsonl
 fi
-if [ -n "$U8PROF" ]; then  # the u8 ingest launch (fir_mxi): kernel trace + FETCH / WRITE PMC
+if [ -n "$U8PROF" ]; then
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_u8 -o run -- python3 $R/bench_configs.py --config c2u8 --steps 20 --warmup 5 > $O/prof_u8.jsonl 2> $O/prof_u8.log || { tail -20 $O/prof_u8.log; exit 10; }
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_u8/pmc_fetch -o run -- python3 $R/bench_configs.py --config c2u8 --steps 3 --warmup 1 > $O/pmc_u8_fetch.log 2>&1 || { tail -5 $O/pmc_u8_fetch.log; exit 11; }

@@ -2,8 +2,8 @@
 """Per-launch durations of a FIR launch from the start of a busy period:
 bench.py's own setup, then every launch bracketed by HIP events on the handle's stream.
 
-    python tools/gpu/r04_series.py [--kind c64|u8|bank] [--clk]
-    python tools/experiments/run_with_lib.py LIB.so tools/gpu/r04_series.py ...   (a variant)
+    python tools/gpu/series.py [--kind c64|u8|bank] [--clk]
+    python tools/experiments/run_with_lib.py LIB.so tools/gpu/series.py ...   (a variant)
 
 Phases (one JSON line each, per-launch ms in "ms"):
   driver   5 warmups + 20 launches: what `bench.py --steps 20 --warmup 5` runs (warmups
