@@ -10,11 +10,14 @@ O=$R/gpurun_out/${OUT:-ab}
 BASE=${BASE:-tools/diag/probe_build/lib_base.so}
 mkdir -p $O
 cd $R
+# ARMS="name=lib.so ..." alternates several builds instead (names without "_"; "new" = product)
+ARMS=${ARMS:-"base=$BASE new=product"}
 for rep in $(seq 1 ${REPS:-3}); do
-  for v in base new; do
+  for arm in $ARMS; do
+    v=${arm%%=*}; lib=${arm#*=}
     for kind in ${KINDS:-c64}; do
-      if [ $v = base ]; then
-        timeout -k 10 120 python -u tools/experiments/run_with_lib.py $BASE tools/gpu/series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
+      if [ $lib != product ]; then
+        timeout -k 10 120 python -u tools/experiments/run_with_lib.py $lib tools/gpu/series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
       else
         timeout -k 10 120 python -u tools/gpu/series.py --kind $kind --long 200 > $O/${v}_${kind}_$rep.jsonl 2> $O/${v}_${kind}_$rep.err || { tail -20 $O/${v}_${kind}_$rep.err; exit 2; }
       fi
