@@ -377,30 +377,44 @@ def bench_c4(args):
     units = nch * n
     fir_check = spot_check(pyoracle, taps, x, mf, nch // 3, n)
     assert fir_check <= 1e-5, fir_check
-    # PLL spot check at the timed width: a fresh handle of the same design (same kernel, all
-    # nch channels) over the first 16 Ki samples of the resident matched-filter output; a few
-    # channels' outputs and lock flags array_equal to the oracle PLL (src/filter/pll.rs:70-85)
-    m = min(n, 1 << 14)
+    # PLL spot check of the timed path (time-parallel segments at this shape): a fresh handle
+    # of the same design and plan over the whole resident matched-filter output; 4 channels'
+    # outputs and lock flags array_equal to the oracle PLL (src/filter/pll.rs:70-85), which
+    # is the serial recurrence
     pll_v = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
                         f.BiquadD.LowPass(20000.0, 0.7)).design(rate, nch=nch)
     pll_v.set_stream(bank.stream())
-    pll_v.process_dev(mf.ptr, n, m, out.ptr, lk.ptr, n)
+    plan = pll_v.time_parallel_plan(n)
+    pll_v.process_dev(mf.ptr, n, n, out.ptr, lk.ptr, n)
     bank.sync()
+    tp_segments, tp_recomputed = pll_v.last_time_parallel()
     p = pyoracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
     chans = sorted({0, nch // 3, nch // 2 + 1, nch - 1})
-    mfs = np.stack([mf.download(m, offset_bytes=8 * c * n) for c in chans])
+    mfs = np.stack([mf.download(n, offset_bytes=8 * c * n) for c in chans])
     ref_out, ref_lk = pyoracle.pll_batch(p, mfs, nthreads=len(chans))
-    got_out = np.stack([out.download(m, dtype=np.float32, offset_bytes=4 * c * n) for c in chans])
-    got_lk = np.stack([lk.download(m, dtype=np.uint8, offset_bytes=c * n) for c in chans])
+    got_out = np.stack([out.download(n, dtype=np.float32, offset_bytes=4 * c * n) for c in chans])
+    got_lk = np.stack([lk.download(n, dtype=np.uint8, offset_bytes=c * n) for c in chans])
     pll_mism = int(np.sum(got_out != ref_out) + np.sum(got_lk != ref_lk))
     assert pll_mism == 0, f"c4 PLL spot check: {pll_mism} outputs / lock flags differ"
+    m = n
+    # the serial kernel on the same data, for reference (one pass)
+    pll_s = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
+                        f.BiquadD.LowPass(20000.0, 0.7)).design(rate, nch=nch)
+    pll_s.set_stream(bank.stream())
+    pll_s.set_time_parallel(-1)
+    _, ms_serial = time_events(lambda: pll_s.process_dev(mf.ptr, n, n, out.ptr, lk.ptr, n),
+                               bank.stream(), 1, 0, lambda: (bank.sync(), synchronize()))
     res = {"config": f"c4: 255-tap matched filter + PLL FM demod (src/main.rs:41-46), {nch} ch x 2^{args.c4_log2n}",
            "metric": "complex Msamples/s (input, all channels)", "value": round(units / (ms * 1e-3) / 1e6, 1),
            "roofline": roof(12, units, ms), "fir_ms": round(ms_fir, 3), "pll_ms": round(ms - ms_fir, 3),
            "pll_ns_per_sample_chain": round((ms - ms_fir) * 1e6 / n, 2),
-           "note": "PLL is bound by its loop-carried latency (ns per sample per channel chain), not HBM",
+           "pll_plan": {"segment": plan[0], "warm": plan[1], "segments_per_channel": tp_segments,
+                        "segments_recomputed": tp_recomputed},
+           "pll_serial_ms": round(ms_serial, 3),
+           "pll_serial_ns_per_sample_chain": round(ms_serial * 1e6 / n, 2),
+           "note": "the PLL recurrence is serial per channel; time-parallel segments (speculative warm-up, exact verification, DESIGN.md 3.6) spread a channel over many SIMDs -- pll_ns_per_sample_chain is the wall time per sample of the whole batch",
            "wall_ms_per_step": round(wall * 1e3, 3), "fir_spot_check_max_over_rms": fir_check,
-           "pll_spot_check": f"channels {chans} x {m} samples: outputs + lock flags array_equal to the oracle"}
+           "pll_spot_check": f"channels {chans} x {m} samples (the whole stream, time-parallel plan {plan}): outputs + lock flags array_equal to the oracle"}
     if not args.no_cpu_baseline:
         cores = min(os.cpu_count() or 1, 16)
         cn, cl = cores, 1 << 14

@@ -291,6 +291,18 @@ int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode);
  * (src/main.rs:48-49 feeds rtl.listen() straight into the PLL), converted in the load as
  * RtlTcpSignal::next does, (v - 128) / 128 (src/rtltcp.rs:156-164); ld_in counts samples. */
 int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind);
+/* Time-parallel blocks (no reference counterpart; results are the serial PLL's bit for bit):
+ * each channel's block is cut into segments of `seg` samples that run concurrently, each after
+ * `warm` samples of warm-up from the design state; a segment whose warm-up did not reach the
+ * true state exactly is recomputed from it.  seg = 0: automatic (enough
+ * segments to give every SIMD one wave, none shorter than the warm-up), seg < 0: always one
+ * serial pass; warm = 0: 16384.  Lengths round up to multiples of 8. */
+int sdrgpu_pll_set_time_parallel(sdrgpu_pll* h, long seg, long warm);
+/* The segment length (0 = one serial pass) and warm-up a block of n samples would use. */
+int sdrgpu_pll_time_parallel_plan(const sdrgpu_pll* h, size_t n, long* seg, long* warm);
+/* The most recent block: its segment count (0 = serial) and how many segments had to be
+ * recomputed from the true state (waits for the handle's stream). */
+int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recomputed);
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
 int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** hip_stream);
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,

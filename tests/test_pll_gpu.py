@@ -304,3 +304,98 @@ def test_pll_special_operands_bit_exact(sdr, oracle):
             bad = (g != r) & ~(np.isnan(out[c]) & np.isnan(ref_out[c]))
             assert not bad.any(), (f"ld={ld} {name}: {bad.sum()} outputs differ, first at "
                                    f"{np.flatnonzero(bad)[0]}")
+
+
+# ---- time-parallel blocks (pll.hip "speculative segments"): bit-identical to the serial PLL ----
+
+@pytest.mark.parametrize("seg,warm", [(4096, 4096), (2048, 64), (8192, 16384), (1000, 512)],
+                         ids=["converging", "mostly-recomputed", "warm-reaches-start", "ragged"])
+def test_pll_time_parallel_bit_exact(sdr, oracle, seg, warm):
+    """main.rs PLL (src/main.rs:41-46; src/filter/pll.rs:70-85) over 96 FM channels with each
+    block cut into concurrent segments: with a warm-up long enough for most segments to reach
+    the true state (converging), one so short that almost every segment is recomputed from the
+    true state, one reaching back to sample 0, and a segment length that is not a multiple of
+    8 (rounded up) with a ragged last segment.  Outputs and lock flags array_equal to the oracle
+    (the serial reference), over two calls (state carried) and against the serial kernel."""
+    rng = np.random.default_rng(700 + seg + warm)
+    nch, n = 96, 30011
+    x = fm_channels(rng, nch, n)
+    pll = main_rs_design(sdr).design(RATE, nch=nch)
+    pll.set_time_parallel(seg, warm)
+    s_plan, w_plan = pll.time_parallel_plan(20000)
+    assert s_plan == (seg + 7) // 8 * 8 and w_plan == warm
+    o1, l1 = pll.process(x[:, :20000])
+    segs, rec = pll.last_time_parallel()
+    assert segs == -(-20000 // s_plan) and 0 <= rec <= nch * (segs - 1)
+    if warm >= 20000 - s_plan:      # every warm-up reaches back to sample 0: exact by construction
+        assert rec == 0
+    if warm == 64:                  # far too short to converge: the fix path carries the block
+        assert rec > nch
+    o2, l2 = pll.process(x[:, 20000:])
+    out, lk = np.concatenate([o1, o2], axis=1), np.concatenate([l1, l2], axis=1)
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)
+    check(out, lk, ref_out, ref_lk, f"time-parallel seg {seg} warm {warm}")
+    serial = main_rs_design(sdr).design(RATE, nch=nch)
+    serial.set_time_parallel(-1)
+    assert serial.time_parallel_plan(n) == (0, 16384)
+    so, sl = serial.process(x)
+    assert np.array_equal(so, out) and np.array_equal(sl, lk)
+    # the carried state is the serial one too: one more block agrees
+    a, b = pll.process(x[:, :3000]), serial.process(x[:, :3000])
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_pll_time_parallel_other_designs_and_u8(sdr, oracle):
+    """examples/pll.rs's design (output LowPass: an output-filter state in the segments'
+    state), the stereo pilot's output mode (src/main.rs:55-66) and rtl_tcp u8 input, each with
+    forced segments: bit-exact to the oracle / to the serial handle."""
+    f = sdr.filter
+    rng = np.random.default_rng(77)
+    nch, n = 40, 24000
+    x = fm_channels(rng, nch, n)
+    d = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.BiquadD.LowPass(20000.0, 0.7),
+                    f.BiquadD.LowPass(20000.0, 0.7))
+    pll = d.design(RATE, nch=nch)
+    pll.set_time_parallel(3000, 2048)
+    out, lk = pll.process(x)
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle, outf=(1, 20000.0, 0.7)), x, nthreads=16)
+    check(out, lk, ref_out, ref_lk, "examples/pll.rs design, time-parallel")
+    iq = rng.integers(0, 256, size=(nch, 2 * n), dtype=np.uint8)
+    a = main_rs_design(sdr).design(RATE, nch=nch)
+    a.set_time_parallel(4000, 4000)
+    b = main_rs_design(sdr).design(RATE, nch=nch)
+    b.set_time_parallel(-1)
+    oa, la = a.process_u8(iq)
+    ob, lb = b.process_u8(iq)
+    assert np.array_equal(oa, ob) and np.array_equal(la, lb)
+    t = np.arange(n) / 144e3
+    v = (0.3 * np.cos(2 * np.pi * 19000.0 * t[None, :] + rng.uniform(0, 6, (4, 1)))).astype(np.float32)
+    pd = f.PllDesign(19000.0, 0.0002, f.BiquadD.LowPass(200.0, 0.7), f.BiquadD.LowPass(20.0, 0.7),
+                     f.BiquadD.LowPass(20.0, 0.7))
+    p1, p2 = pd.design(144e3, nch=4), pd.design(144e3, nch=4)
+    p1.set_time_parallel(2048, 1024)
+    p2.set_time_parallel(-1)
+    m1, d1, k1 = p1.stereo(v)
+    m2, d2, k2 = p2.stereo(v)
+    assert np.array_equal(d1, d2) and np.array_equal(k1, k2)
+
+
+def test_pll_time_parallel_auto_plan_configs3(sdr, oracle):
+    """The automatic plan at configs[3]'s shape (1024 channels x 2^20: 64 segments of 16 Ki,
+    16 Ki of warm-up, one wave per SIMD), and a 1024-channel block of 2^17 samples through it
+    (auto plan: 8 segments) array_equal to the oracle on 8 channels."""
+    nch = 1024
+    pll = main_rs_design(sdr).design(RATE, nch=nch)
+    assert pll.time_parallel_plan(1 << 20) == (16384, 16384)
+    assert pll.time_parallel_plan(16384) == (0, 16384)     # one segment: serial
+    rng = np.random.default_rng(1024)
+    n = 1 << 17
+    chans = [0, 63, 64, 511, 777, 1000, 1022, 1023]
+    x = np.empty((nch, n), np.complex64)
+    x[:] = fm_channels(rng, 1, n)[0]                           # one waveform everywhere ...
+    x[chans] = fm_channels(rng, len(chans), n)                 # ... and 8 different channels
+    assert pll.time_parallel_plan(n) == (16384, 16384)
+    out, lk = pll.process(x)
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), np.ascontiguousarray(x[chans]), nthreads=8)
+    check(out[chans], lk[chans], ref_out, ref_lk, "configs[3] auto plan")
+    assert np.array_equal(out[1], out[2]) and np.array_equal(out[1], out[1020])

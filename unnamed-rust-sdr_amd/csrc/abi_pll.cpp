@@ -69,6 +69,49 @@ struct sdrgpu_pll {
     StreamSlot stream;
     DevBuf stage_in, stage_out, stage_lock;
     AsyncD2H async;
+    // time-parallel segments (pll.hip): requested segment / warm-up lengths (0 = auto, segment
+    // < 0 = always one serial pass), the device's SIMD count, and the [2][segments][nch] states
+    long tp_seg = 0, tp_warm = 0;
+    long simds = 1024;
+    DevBuf spec_buf;
+    long last_nseg = 0;  // segments of the most recent time-parallel block (0: serial)
+
+    // The plan for a block of n samples.  Auto: enough segments per channel to give every SIMD
+    // one wave (64 channel-segments each), none shorter than the warm-up (16 Ki samples: every
+    // configs[3] channel's state had converged within 12.2 Ki).
+    void plan(long n, long* seg, long* warm) const {
+        *seg = 0;
+        *warm = tp_warm > 0 ? (tp_warm + 7) / 8 * 8 : 16384;
+        if (tp_seg < 0 || n <= 0) return;
+        long sg;
+        if (tp_seg > 0) {
+            sg = (tp_seg + 7) / 8 * 8;
+        } else {
+            const long by_lanes = 64 * simds / dp.nch, by_len = n / *warm;
+            const long nseg = by_lanes < by_len ? by_lanes : by_len;
+            if (nseg < 2) return;
+            sg = ((n + nseg - 1) / nseg + 7) / 8 * 8;
+        }
+        if (n > sg) *seg = sg;
+    }
+
+    int make_spec(long n, PllSpec* sp) {
+        plan(n, &sp->seg, &sp->warm);
+        last_nseg = 0;
+        if (sp->seg <= 0) return SDRGPU_OK;
+        const long nseg = (n + sp->seg - 1) / sp->seg;
+        const size_t bytes = 2 * (size_t)nseg * (size_t)dp.nch * sizeof(PllChannelState) + 64;
+        if (bytes > spec_buf.cap) {  // growing frees a buffer an earlier block may still use
+            SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
+            int st = spec_buf.ensure(bytes);
+            if (st) return st;
+        }
+        sp->guess = static_cast<PllChannelState*>(spec_buf.ptr);
+        sp->end = sp->guess + nseg * dp.nch;
+        sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end + nseg * dp.nch);
+        last_nseg = nseg;
+        return SDRGPU_OK;
+    }
 
     void free_all() {
         DeviceGuard g(device);
@@ -78,6 +121,7 @@ struct sdrgpu_pll {
         stage_in.release();
         stage_out.release();
         stage_lock.release();
+        spec_buf.release();
         stream.destroy();
     }
 };
@@ -119,6 +163,10 @@ int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu
         if (!g.ok()) st = SDRGPU_ERR_DEVICE;
         if (!st) st = h->stream.create();
         if (!st && hipMalloc(&h->d_state, nch * sizeof(PllChannelState)) != hipSuccess) st = SDRGPU_ERR_NOMEM;
+        int cus = 0;
+        if (!st && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+            cus > 0)
+            h->simds = 4L * cus;
     }
     if (!st) st = sdrgpu_pll_reset(h);
     if (st) {
@@ -143,6 +191,34 @@ int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode) {
     return SDRGPU_OK;
 }
 
+int sdrgpu_pll_set_time_parallel(sdrgpu_pll* h, long seg, long warm) {
+    if (!h || warm < 0) return SDRGPU_ERR_INVALID;
+    h->tp_seg = seg;
+    h->tp_warm = warm;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_time_parallel_plan(const sdrgpu_pll* h, size_t n, long* seg, long* warm) {
+    if (!h || !seg || !warm) return SDRGPU_ERR_INVALID;
+    h->plan((long)n, seg, warm);
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recomputed) {
+    if (!h || !segments || !recomputed) return SDRGPU_ERR_INVALID;
+    *segments = h->last_nseg;
+    *recomputed = 0;
+    if (h->last_nseg > 0) {
+        DeviceGuard g(h->device);
+        unsigned long long r = 0;
+        const auto* base = static_cast<const PllChannelState*>(h->spec_buf.ptr);
+        SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+        SDRGPU_HIP_TRY(hipMemcpy(&r, base + 2 * h->last_nseg * h->dp.nch, sizeof(r), hipMemcpyDeviceToHost));
+        *recomputed = (long)r;
+    }
+    return SDRGPU_OK;
+}
+
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* s) {
     if (!h) return SDRGPU_ERR_INVALID;
     h->stream.set(s);
@@ -162,8 +238,11 @@ int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t
     if (!d_in || !d_out || !d_locked || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    PllSpec sp;
+    int st = h->make_spec((long)n, &sp);
+    if (st) return st;
     return pll_launch(h->dp, d_in, (long)ld_in, (long)n, d_out, d_locked,
-                      (long)ld_out, h->d_state, h->stream.cur);
+                      (long)ld_out, h->d_state, sp, h->stream.cur);
 }
 
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, float* out,
@@ -180,11 +259,13 @@ int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, fl
         (st = h->stage_out.ensure(nch * n * sizeof(float))) ||
         (st = h->stage_lock.ensure(nch * n)))
         return st;
+    PllSpec sp;
+    if ((st = h->make_spec((long)n, &sp))) return st;
     SDRGPU_HIP_TRY(hipMemcpy2DAsync(h->stage_in.ptr, n * sb, in, ld_in * sb, n * sb, nch,
                                     hipMemcpyHostToDevice, h->stream.cur));
     if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n,
                          static_cast<float*>(h->stage_out.ptr), static_cast<uint8_t*>(h->stage_lock.ptr),
-                         (long)n, h->d_state, h->stream.cur)))
+                         (long)n, h->d_state, sp, h->stream.cur)))
         return st;
     SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(float), h->stage_out.ptr, n * sizeof(float),
                                     n * sizeof(float), nch, hipMemcpyDeviceToHost, h->stream.cur));
@@ -214,8 +295,10 @@ int sdrgpu_pll_process_async(sdrgpu_pll* h, const void* in, size_t n, float* out
                                   h->stream.cur));
     float* d_out = static_cast<float*>(h->async.out[slot][0].ptr);
     uint8_t* d_lock = static_cast<uint8_t*>(h->async.out[slot][1].ptr);
+    PllSpec sp;
+    if ((st = h->make_spec((long)n, &sp))) return st;
     if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n, d_out, d_lock, (long)n,
-                         h->d_state, h->stream.cur)))
+                         h->d_state, sp, h->stream.cur)))
         return st;
     if ((st = h->async.begin_download(h->stream.cur, slot))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(out, d_out, ob[0], hipMemcpyDeviceToHost, h->async.d2h));
@@ -250,6 +333,8 @@ int sdrgpu_pll_clone(const sdrgpu_pll* h, sdrgpu_pll** out) {
     if (st) return st;
     (*out)->dp.out_mode = h->dp.out_mode;
     (*out)->dp.in_u8 = h->dp.in_u8;
+    (*out)->tp_seg = h->tp_seg;
+    (*out)->tp_warm = h->tp_warm;
     DeviceGuard g(h->device);
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
     SDRGPU_HIP_TRY(hipMemcpy((*out)->d_state, h->d_state, h->dp.nch * sizeof(PllChannelState),

@@ -20,6 +20,7 @@
 // Mul, Biquad::apply's `0 + v*b0 + x1*b1 + ...`), and sin/cos/atan2 are the bit-exact
 // restatements of the glibc functions Rust std calls (libm_glibc.h).
 #include <algorithm>
+#include <cstddef>
 #include <type_traits>
 
 #include "common.hpp"
@@ -72,39 +73,25 @@ __device__ __forceinline__ float bq_real(const Bq& c, float x, float& x1, float&
 // reference's callers are compiled as their own kernels (src/main.rs:41-46: loop LowPass,
 // output Identity, lock LowPass; examples/pll.rs:9-15: three LowPass; the stereo pilot
 // src/main.rs:55-60), so no per-sample control flow is left in them.
-// VEC: the channel's rows are 16-B aligned with ld_in even / ld_out a multiple of 8, so a
-// chunk of 8 samples moves in 4 (c64) or 1 (u8) loads and 3 stores.
-template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
-__global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const void* __restrict__ in_,
-                                                        long ld_in, long n, float* __restrict__ out,
-                                                        uint8_t* __restrict__ locked, long ld_out,
-                                                        PllChannelState* __restrict__ state) {
-    own_simd();
-    const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
-    if (ch >= p.nch) return;
-    PllChannelState s = state[ch];
-    const float2* __restrict__ xf = static_cast<const float2*>(in_) + ch * ld_in;
-    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(in_) + ch * ld_in;
-    auto cvt = [](unsigned w) -> float2 {
-        return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);
-    };
-    auto ld = [&](long i) -> float2 {
-        if constexpr (U8) return cvt(xu[i]);
-        else return xf[i];
-    };
-    float* __restrict__ y = out + ch * ld_out;
-    uint8_t* __restrict__ lk = locked + ch * ld_out;
-    const Bq L = {p.loopc[0], p.loopc[1], p.loopc[2], p.loopc[3], p.loopc[4]};
-    const Bq O = {p.outc[0], p.outc[1], p.outc[2], p.outc[3], p.outc[4]};
-    const Bq K = {p.lockc[0], p.lockc[1], p.lockc[2], p.lockc[3], p.lockc[4]};
-    const bool loop_id = LID == 2 ? p.loop_ident != 0 : LID == 1;
-    const bool out_id = OID == 2 ? p.out_ident != 0 : OID == 1;
-    const bool lock_id = KID == 2 ? p.lock_ident != 0 : KID == 1;
-    const int mode = MODE == 2 ? p.out_mode : MODE;
-    constexpr float kTwoPi = 2.0f * 3.14159265358979323846f;  // 2.0 * f32::consts::PI
+template <int LID, int OID, int KID, int MODE>
+struct PllLane {
+    Bq L, O, K;
+    float gain, reference, rate;
+    bool loop_id, out_id, lock_id;
+    int mode;
+    __device__ explicit PllLane(const PllDevParams& p)
+        : L{p.loopc[0], p.loopc[1], p.loopc[2], p.loopc[3], p.loopc[4]},
+          O{p.outc[0], p.outc[1], p.outc[2], p.outc[3], p.outc[4]},
+          K{p.lockc[0], p.lockc[1], p.lockc[2], p.lockc[3], p.lockc[4]},
+          gain(p.gain), reference(p.reference), rate(p.rate),
+          loop_id(LID == 2 ? p.loop_ident != 0 : LID == 1),
+          out_id(OID == 2 ? p.out_ident != 0 : OID == 1),
+          lock_id(KID == 2 ? p.lock_ident != 0 : KID == 1),
+          mode(MODE == 2 ? p.out_mode : MODE) {}
 
     // one reference Pll::apply step; returns (output or 0, locked)
-    auto step = [&](float2 v, float& ov, uint8_t& lv) {
+    __device__ __forceinline__ void step(PllChannelState& s, float2 v, float& ov, uint8_t& lv) const {
+        constexpr float kTwoPi = 2.0f * 3.14159265358979323846f;  // 2.0 * f32::consts::PI
         // c = value * conj(self.value)  (pll.rs:71; num-complex 0.2 Mul)
         const float cjr = s.vr, cji = -s.vi;
         const float cr = v.x * cjr - v.y * cji;
@@ -123,8 +110,8 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
             lr = orr;
             li = oi;
         }
-        const float phasedif = sdr_atan2f_bfx(li, lr) * p.gain;   // :72 arg() * gain
-        float nph = s.nphase + (p.reference + phasedif);           // :73
+        const float phasedif = sdr_atan2f_bfx(li, lr) * gain;     // :72 arg() * gain
+        float nph = s.nphase + (reference + phasedif);             // :73
         nph = nph - truncf(nph);                                   // :74 fract()
         s.nphase = nph;
         const float phase = kTwoPi * nph;                          // :75
@@ -134,8 +121,8 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         s.vi = 1.0f * sn;
         // off the loop-carried chain: lock / output filters and the output select
         const float lockv = lock_id ? cr : bq_real(K, cr, s.kx1, s.kx2, s.ky1, s.ky2);  // :78
-        const float o = out_id ? phasedif * p.rate
-                               : bq_real(O, phasedif * p.rate, s.ox1, s.ox2, s.oy1, s.oy2);
+        const float o = out_id ? phasedif * rate
+                               : bq_real(O, phasedif * rate, s.ox1, s.ox2, s.oy1, s.oy2);
         const bool lockd = lockv > 0.01f;                          // :80
         lv = lockd ? 1 : 0;
         if (mode == 1) {
@@ -150,12 +137,31 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         } else {
             ov = lockd ? o : 0.0f;
         }
-    };
+    }
+};
 
-    // full chunks of kChunk samples, the next chunk's loads in flight
+__device__ __forceinline__ float2 cvt_u8(unsigned w) {
+    return make_float2(((float)(w & 255u) - 128.0f) / 128.0f, ((float)((w >> 8) & 255u) - 128.0f) / 128.0f);
+}
+
+// Samples [a, b) of one channel row through the step.  STORE: outputs and lock flags to y / lk
+// (indexed like the input); otherwise only the state advances (a warm-up).  VEC: the row is
+// 16-B aligned (ld_in even, or a multiple of 8 for u8 input), a is a multiple of kChunk and
+// y / lk are 16-B / 8-B aligned at a multiple of kChunk, so a chunk of 8 samples moves in 4
+// (c64) or 1 (u8) loads and 3 stores, the next chunk's loads in flight.
+template <bool U8, bool VEC, bool STORE, class Lane>
+__device__ __forceinline__ void pll_run(const Lane& ln, PllChannelState& s, const void* __restrict__ row,
+                                        long a, long b, float* __restrict__ y,
+                                        uint8_t* __restrict__ lk) {
+    const float2* __restrict__ xf = static_cast<const float2*>(row);
+    const unsigned short* __restrict__ xu = static_cast<const unsigned short*>(row);
+    auto ld = [&](long i) -> float2 {
+        if constexpr (U8) return cvt_u8(xu[i]);
+        else return xf[i];
+    };
     using RawT = std::conditional_t<U8, uint4, float4>;
     constexpr int NR = U8 ? 1 : kChunk / 2;  // raw vector loads per chunk
-    const long nfull = n / kChunk * kChunk;
+    const long bfull = a + (b - a) / kChunk * kChunk;
     RawT raw[NR];
     auto ldc = [&](long i) {  // chunk starting at sample i
         if constexpr (VEC) {
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         if constexpr (VEC) {
             if constexpr (U8) {
                 const unsigned w = (&raw[0].x)[k >> 1];
-                return cvt((k & 1) ? (w >> 16) : (w & 0xffffu));
+                return cvt_u8((k & 1) ? (w >> 16) : (w & 0xffffu));
             } else {
                 const float4 r = raw[k >> 1];
                 return (k & 1) ? make_float2(r.z, r.w) : make_float2(r.x, r.y);
@@ -178,16 +184,16 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         }
     };
     float2 buf[kChunk];
-    if (nfull > 0) {
-        ldc(0);
+    if (bfull > a) {
+        ldc(a);
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) buf[k] = sample(k, 0);
+        for (int k = 0; k < kChunk; ++k) buf[k] = sample(k, a);
     }
-    for (long i = 0; i < nfull; i += kChunk) {
+    for (long i = a; i < bfull; i += kChunk) {
         float2 cur[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) cur[k] = buf[k];
-        if (i + kChunk < nfull) {  // prefetch
+        if (i + kChunk < bfull) {  // prefetch
             ldc(i + kChunk);
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) buf[k] = sample(k, i + kChunk);
@@ -195,32 +201,119 @@ __global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const vo
         float ov[kChunk];
         uint8_t lv[kChunk];
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) step(cur[k], ov[k], lv[k]);
-        if constexpr (VEC) {
-            float4* yo = reinterpret_cast<float4*>(y + i);
-            yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
-            yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
-            uint2 pk;
-            pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
-            pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
-            *reinterpret_cast<uint2*>(lk + i) = pk;
-        } else {
+        for (int k = 0; k < kChunk; ++k) ln.step(s, cur[k], ov[k], lv[k]);
+        if constexpr (STORE) {
+            if constexpr (VEC) {
+                float4* yo = reinterpret_cast<float4*>(y + i);
+                yo[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+                yo[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
+                uint2 pk;
+                pk.x = lv[0] | (lv[1] << 8) | (lv[2] << 16) | ((unsigned)lv[3] << 24);
+                pk.y = lv[4] | (lv[5] << 8) | (lv[6] << 16) | ((unsigned)lv[7] << 24);
+                *reinterpret_cast<uint2*>(lk + i) = pk;
+            } else {
 #pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                y[i + k] = ov[k];
-                lk[i + k] = lv[k];
+                for (int k = 0; k < kChunk; ++k) {
+                    y[i + k] = ov[k];
+                    lk[i + k] = lv[k];
+                }
             }
         }
     }
-    // ragged tail: exactly n - nfull more samples (the state must not see padding)
-    for (long i = nfull; i < n; ++i) {
+    // ragged tail: exactly b - bfull more samples (the state must not see padding)
+    for (long i = bfull; i < b; ++i) {
         float o;
         uint8_t l;
-        step(ld(i), o, l);
-        y[i] = o;
-        lk[i] = l;
+        ln.step(s, ld(i), o, l);
+        if constexpr (STORE) {
+            y[i] = o;
+            lk[i] = l;
+        }
     }
+}
+
+template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
+__global__ __launch_bounds__(kPllBlock) void pll_kernel(PllDevParams p, const void* __restrict__ in_,
+                                                        long ld_in, long n, float* __restrict__ out,
+                                                        uint8_t* __restrict__ locked, long ld_out,
+                                                        PllChannelState* __restrict__ state) {
+    own_simd();
+    const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
+    if (ch >= p.nch) return;
+    PllChannelState s = state[ch];
+    const PllLane<LID, OID, KID, MODE> ln(p);
+    const void* row = static_cast<const char*>(in_) + ch * ld_in * (U8 ? 2 : 8);
+    pll_run<U8, VEC, true>(ln, s, row, 0, n, out + ch * ld_out, locked + ch * ld_out);
     state[ch] = s;
+}
+
+// Time-parallel PLL ("speculative segments").  The recurrence is serial, but a PLL that is
+// tracking forgets its initial state: from any start, the whole state (NCO phase and value,
+// loop / lock / output filter states) comes to agree BIT FOR BIT with the true trajectory after
+// a few thousand samples of the same input (configs[3]'s FM channels: median 3.4 k, max 12 k
+// samples in 128 channels).  So each channel's block is cut into segments that
+// run at once, one lane each (pll_seg_kernel): a segment first runs `warm` samples of warm-up
+// from the design state (no outputs), records the state it reached at its start (guess), then
+// produces its outputs and records its end state.  pll_fix_kernel (one lane per channel) then
+// walks the segments in order with the TRUE state (segment 0 starts from the carried state;
+// so does every segment whose warm-up reaches back to sample 0): where a segment's guess equals
+// the true state bit for bit, its outputs are exactly the serial ones (same state, same inputs,
+// same arithmetic) and its end state is true; where it differs, the segment is recomputed from
+// the true state.  Every output is therefore the serial PLL's; only the time depends on how
+// many segments have to be recomputed (none, typically; all of them for a chaotic, unlocked
+// loop, which then costs one serial pass more than pll_kernel).
+template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
+__global__ __launch_bounds__(kPllBlock) void pll_seg_kernel(
+    PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
+    uint8_t* __restrict__ locked, long ld_out, const PllChannelState* __restrict__ state, long seg,
+    long warm, long nseg, PllChannelState* __restrict__ guess, PllChannelState* __restrict__ endst) {
+    own_simd();
+    const long g = (long)blockIdx.x * kPllBlock + threadIdx.x;
+    if (g >= p.nch * nseg) return;
+    const long ch = g % p.nch, sg = g / p.nch;
+    const long t0 = sg * seg, t1 = t0 + seg < n ? t0 + seg : n, tw = t0 > warm ? t0 - warm : 0;
+    PllChannelState s{};  // PllDesign::design's state (pll.rs:57-58) unless the warm-up starts at 0
+    if (tw == 0) s = state[ch];
+    const PllLane<LID, OID, KID, MODE> ln(p);
+    const void* row = static_cast<const char*>(in_) + ch * ld_in * (U8 ? 2 : 8);
+    pll_run<U8, VEC, false>(ln, s, row, tw, t0, nullptr, nullptr);
+    guess[g] = s;
+    pll_run<U8, VEC, true>(ln, s, row, t0, t1, out + ch * ld_out, locked + ch * ld_out);
+    endst[g] = s;
+}
+
+__device__ __forceinline__ bool same_state(const PllChannelState& a, const PllChannelState& b) {
+    const unsigned* x = reinterpret_cast<const unsigned*>(&a);
+    const unsigned* y = reinterpret_cast<const unsigned*>(&b);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < (int)(offsetof(PllChannelState, pad) / sizeof(float)); ++i) eq &= x[i] == y[i];
+    return eq;
+}
+
+template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
+__global__ __launch_bounds__(kPllBlock) void pll_fix_kernel(
+    PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
+    uint8_t* __restrict__ locked, long ld_out, PllChannelState* __restrict__ state, long seg,
+    long warm, long nseg, const PllChannelState* __restrict__ guess,
+    const PllChannelState* __restrict__ endst, unsigned long long* __restrict__ recomputed) {
+    own_simd();
+    const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
+    if (ch >= p.nch) return;
+    const PllLane<LID, OID, KID, MODE> ln(p);
+    const void* row = static_cast<const char*>(in_) + ch * ld_in * (U8 ? 2 : 8);
+    PllChannelState t = endst[ch];  // segment 0 started from the carried state: exact
+    for (long sg = 1; sg < nseg; ++sg) {
+        const long t0 = sg * seg, t1 = t0 + seg < n ? t0 + seg : n;
+        const long g = sg * p.nch + ch;
+        if (t0 <= warm || same_state(guess[g], t)) {
+            t = endst[g];
+        } else {  // the warm-up did not reach the true state: this segment again, from it
+            pll_run<U8, VEC, true>(ln, t, row, t0, t1, out + ch * ld_out, locked + ch * ld_out);
+            atomicAdd(recomputed, 1ull);
+        }
+    }
+    state[ch] = t;
 }
 
 // Output modes 0 and 1 with vector rows (configs[3]'s 1024 channels, main.rs's single
@@ -392,12 +485,27 @@ __global__ __launch_bounds__(2 * kPllBlock) void pll_split_kernel(
 
 template <bool U8, int LID, int OID, int KID, int MODE>
 void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
-                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
+                uint8_t* locked, long ld_out, PllChannelState* state, const PllSpec& spec,
+                hipStream_t s) {
     const long nblk = (p.nch + kPllBlock - 1) / kPllBlock;
     const size_t sb = U8 ? 2 : 8;
     const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in * sb) % 16 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (ld_out % 8) == 0 &&
                      (reinterpret_cast<uintptr_t>(locked) & 7) == 0;
+    if (spec.seg > 0 && n > spec.seg) {  // time-parallel segments (seg, warm multiples of kChunk)
+        const long nseg = (n + spec.seg - 1) / spec.seg;
+        const long sblk = (p.nch * nseg + kPllBlock - 1) / kPllBlock;
+#define SDRGPU_PLL_SEG(V)                                                                          \
+        hipLaunchKernelGGL((pll_seg_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),      \
+                           dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
+                           spec.seg, spec.warm, nseg, spec.guess, spec.end);                        \
+        hipLaunchKernelGGL((pll_fix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)nblk),      \
+                           dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
+                           spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.recomputed)
+        if (vec) { SDRGPU_PLL_SEG(true); } else { SDRGPU_PLL_SEG(false); }
+#undef SDRGPU_PLL_SEG
+        return;
+    }
     if (vec && (MODE == 0 || MODE == 1))
         hipLaunchKernelGGL((pll_split_kernel<U8, LID, OID, KID, MODE>), dim3((unsigned)nblk),
                            dim3(2 * kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state);
@@ -411,16 +519,17 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
 
 template <bool U8>
 void launch_any(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
-                uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
+                uint8_t* locked, long ld_out, PllChannelState* state, const PllSpec& spec,
+                hipStream_t s) {
     const int l = p.loop_ident, o = p.out_ident, k = p.lock_ident, m = p.out_mode;
     if (!l && o && !k && m == 0)            // src/main.rs:41-46
-        launch_cfg<U8, 0, 1, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, s);
+        launch_cfg<U8, 0, 1, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
     else if (!l && !o && !k && m == 0)      // examples/pll.rs:9-15
-        launch_cfg<U8, 0, 0, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, s);
+        launch_cfg<U8, 0, 0, 0, 0>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
     else if (!l && !o && !k && m == 1)      // the stereo pilot, src/main.rs:55-66
-        launch_cfg<U8, 0, 0, 0, 1>(p, in, ld_in, n, out, locked, ld_out, state, s);
+        launch_cfg<U8, 0, 0, 0, 1>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
     else
-        launch_cfg<U8, 2, 2, 2, 2>(p, in, ld_in, n, out, locked, ld_out, state, s);
+        launch_cfg<U8, 2, 2, 2, 2>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
 }
 
 }  // namespace
@@ -456,10 +565,16 @@ int libm_debug_launch(int fn, const float* a, const float* b, float* o0, float* 
 }
 
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
-               uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s) {
+               uint8_t* locked, long ld_out, PllChannelState* state, const PllSpec& spec,
+               hipStream_t s) {
     if (n <= 0) return SDRGPU_OK;
-    if (p.in_u8) launch_any<true>(p, in, ld_in, n, out, locked, ld_out, state, s);
-    else launch_any<false>(p, in, ld_in, n, out, locked, ld_out, state, s);
+    if (spec.seg > 0 && (spec.seg % kChunk || spec.warm % kChunk || !spec.guess || !spec.end ||
+                         !spec.recomputed))
+        return SDRGPU_ERR_INVALID;
+    if (spec.seg > 0 && n > spec.seg)
+        SDRGPU_HIP_TRY(hipMemsetAsync(spec.recomputed, 0, sizeof(unsigned long long), s));
+    if (p.in_u8) launch_any<true>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
+    else launch_any<false>(p, in, ld_in, n, out, locked, ld_out, state, spec, s);
     SDRGPU_LAUNCH_CHECK();
     return SDRGPU_OK;
 }

@@ -25,8 +25,20 @@ struct PllChannelState {
     float pad;
 };
 
+// Time-parallel plan of one block (pll.hip, "speculative segments"): seg > 0 cuts each
+// channel's n samples into ceil(n / seg) segments run concurrently, each after `warm` samples
+// of warm-up from the design state; guess / end hold [segments][nch] states (the state each
+// segment's warm-up reached at its start, and the state at its end).  seg == 0: one serial pass.
+struct PllSpec {
+    long seg = 0, warm = 0;
+    PllChannelState* guess = nullptr;
+    PllChannelState* end = nullptr;
+    unsigned long long* recomputed = nullptr;  // segments pll_fix_kernel ran again (zeroed per block)
+};
+
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
-               uint8_t* locked, long ld_out, PllChannelState* state, hipStream_t s);
+               uint8_t* locked, long ld_out, PllChannelState* state, const PllSpec& spec,
+               hipStream_t s);
 
 // test-only: the device atan2f (fn 0) / sincosf (fn 1) restatements over n operands
 int libm_debug_launch(int fn, const float* a, const float* b, float* o0, float* o1, long n,

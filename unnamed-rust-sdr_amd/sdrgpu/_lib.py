@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint8, c_uint32, c_void_p
+from ctypes import POINTER, c_char_p, c_float, c_int, c_long, c_size_t, c_uint8, c_uint32, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "libsdrgpu.so")
@@ -163,6 +163,9 @@ SIGNATURES = [
     ("sdrgpu_pll_create", c_int, [c_int, POINTER(PllParamsC), c_size_t, _PH]),
     ("sdrgpu_pll_set_output_mode", c_int, [_H, c_int]),
     ("sdrgpu_pll_set_input_kind", c_int, [_H, c_int]),
+    ("sdrgpu_pll_set_time_parallel", c_int, [_H, c_long, c_long]),
+    ("sdrgpu_pll_time_parallel_plan", c_int, [_H, c_size_t, POINTER(c_long), POINTER(c_long)]),
+    ("sdrgpu_pll_last_time_parallel", c_int, [_H, POINTER(c_long), POINTER(c_long)]),
     ("sdrgpu_pll_set_stream", c_int, [_H, c_void_p]),
     ("sdrgpu_pll_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_pll_process", c_int,

@@ -496,6 +496,25 @@ class Pll:
             self.set_output_mode(_lib.PLL_OUT_FILTER)
         return v * np.float32(0.5), diff, locked
 
+    def set_time_parallel(self, seg: int = 0, warm: int = 0):
+        """Time-parallel blocks (bit-identical results): seg = 0 automatic, < 0 off (one serial
+        pass), > 0 a forced segment length; warm = warm-up samples (0: 16384)."""
+        check(lib().sdrgpu_pll_set_time_parallel(self._h, seg, warm), "sdrgpu_pll_set_time_parallel")
+
+    def last_time_parallel(self):
+        """(segments, segments recomputed) of the most recent block (0, 0 when serial)."""
+        a, b = ctypes.c_long(), ctypes.c_long()
+        check(lib().sdrgpu_pll_last_time_parallel(self._h, ctypes.byref(a), ctypes.byref(b)),
+              "sdrgpu_pll_last_time_parallel")
+        return a.value, b.value
+
+    def time_parallel_plan(self, n: int):
+        """(segment length or 0 for one serial pass, warm-up) for a block of n samples."""
+        seg, warm = ctypes.c_long(), ctypes.c_long()
+        check(lib().sdrgpu_pll_time_parallel_plan(self._h, n, ctypes.byref(seg), ctypes.byref(warm)),
+              "sdrgpu_pll_time_parallel_plan")
+        return seg.value, warm.value
+
     def set_stream(self, stream_ptr):
         check(lib().sdrgpu_pll_set_stream(self._h, stream_ptr), "sdrgpu_pll_set_stream")
 
