@@ -75,6 +75,7 @@ struct sdrgpu_pll {
     long simds = 1024;
     DevBuf spec_buf;
     long last_nseg = 0;  // segments of the most recent time-parallel block (0: serial)
+    long last_nck = 0;   // and the checkpoints per segment it kept
 
     // The plan for a block of n samples.  Auto: enough segments per channel to give every SIMD
     // one wave (64 channel-segments each), none shorter than the warm-up (16 Ki samples: every
@@ -100,7 +101,14 @@ struct sdrgpu_pll {
         last_nseg = 0;
         if (sp->seg <= 0) return SDRGPU_OK;
         const long nseg = (n + sp->seg - 1) / sp->seg;
-        const size_t bytes = 2 * (size_t)nseg * (size_t)dp.nch * sizeof(PllChannelState) + 64;
+        // checkpoints every ck samples: at most 16 per segment, ck a multiple of 8 dividing seg
+        long ck = sp->seg;
+        for (long d = 16; d >= 2; --d)
+            if (sp->seg % (8 * d) == 0 && sp->seg / d >= 1024) { ck = sp->seg / d; break; }
+        sp->ck = ck;
+        const size_t nck = (size_t)(sp->seg / ck - 1);
+        const size_t nstate = (size_t)nseg * (size_t)dp.nch;
+        const size_t bytes = (2 + nck) * nstate * sizeof(PllChannelState) + 64;
         if (bytes > spec_buf.cap) {  // growing frees a buffer an earlier block may still use
             SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
             int st = spec_buf.ensure(bytes);
@@ -108,8 +116,10 @@ struct sdrgpu_pll {
         }
         sp->guess = static_cast<PllChannelState*>(spec_buf.ptr);
         sp->end = sp->guess + nseg * dp.nch;
-        sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end + nseg * dp.nch);
+        sp->ckpt = nck ? sp->end + nstate : nullptr;
+        sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end + nstate + nck * nstate);
         last_nseg = nseg;
+        last_nck = (long)nck;
         return SDRGPU_OK;
     }
 
@@ -213,7 +223,8 @@ int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recompute
         unsigned long long r = 0;
         const auto* base = static_cast<const PllChannelState*>(h->spec_buf.ptr);
         SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
-        SDRGPU_HIP_TRY(hipMemcpy(&r, base + 2 * h->last_nseg * h->dp.nch, sizeof(r), hipMemcpyDeviceToHost));
+        SDRGPU_HIP_TRY(hipMemcpy(&r, base + (2 + h->last_nck) * h->last_nseg * h->dp.nch, sizeof(r),
+                                 hipMemcpyDeviceToHost));
         *recomputed = (long)r;
     }
     return SDRGPU_OK;

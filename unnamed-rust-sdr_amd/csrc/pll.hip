@@ -266,7 +266,8 @@ template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
 __global__ __launch_bounds__(kPllBlock) void pll_seg_kernel(
     PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
     uint8_t* __restrict__ locked, long ld_out, const PllChannelState* __restrict__ state, long seg,
-    long warm, long nseg, PllChannelState* __restrict__ guess, PllChannelState* __restrict__ endst) {
+    long warm, long nseg, PllChannelState* __restrict__ guess, PllChannelState* __restrict__ endst,
+    long ck, PllChannelState* __restrict__ ckpt) {
     own_simd();
     const long g = (long)blockIdx.x * kPllBlock + threadIdx.x;
     if (g >= p.nch * nseg) return;
@@ -278,7 +279,16 @@ __global__ __launch_bounds__(kPllBlock) void pll_seg_kernel(
     const void* row = static_cast<const char*>(in_) + ch * ld_in * (U8 ? 2 : 8);
     pll_run<U8, VEC, false>(ln, s, row, tw, t0, nullptr, nullptr);
     guess[g] = s;
-    pll_run<U8, VEC, true>(ln, s, row, t0, t1, out + ch * ld_out, locked + ch * ld_out);
+    // the segment in checkpoint intervals: a recomputation from the true state can stop where
+    // it meets this trajectory (pll_fix_kernel)
+    const long nck = seg / ck;
+    PllChannelState* __restrict__ cp = ckpt + g * (nck - 1);
+    for (long j = 0; j < nck; ++j) {
+        const long a = t0 + j * ck, b = j + 1 < nck ? (a + ck < t1 ? a + ck : t1) : t1;
+        if (a >= b) break;
+        pll_run<U8, VEC, true>(ln, s, row, a, b, out + ch * ld_out, locked + ch * ld_out);
+        if (j + 1 < nck) cp[j] = s;
+    }
     endst[g] = s;
 }
 
@@ -296,7 +306,8 @@ __global__ __launch_bounds__(kPllBlock) void pll_fix_kernel(
     PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
     uint8_t* __restrict__ locked, long ld_out, PllChannelState* __restrict__ state, long seg,
     long warm, long nseg, const PllChannelState* __restrict__ guess,
-    const PllChannelState* __restrict__ endst, unsigned long long* __restrict__ recomputed) {
+    const PllChannelState* __restrict__ endst, unsigned long long* __restrict__ recomputed, long ck,
+    const PllChannelState* __restrict__ ckpt) {
     own_simd();
     const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
     if (ch >= p.nch) return;
@@ -308,8 +319,18 @@ __global__ __launch_bounds__(kPllBlock) void pll_fix_kernel(
         const long g = sg * p.nch + ch;
         if (t0 <= warm || same_state(guess[g], t)) {
             t = endst[g];
-        } else {  // the warm-up did not reach the true state: this segment again, from it
-            pll_run<U8, VEC, true>(ln, t, row, t0, t1, out + ch * ld_out, locked + ch * ld_out);
+        } else {  // the warm-up did not reach the true state: this segment again, from it, up
+                  // to the first checkpoint its trajectory meets (from there on it is exact)
+            const long nck = seg / ck;
+            const PllChannelState* __restrict__ cp = ckpt + g * (nck - 1);
+            bool met = false;
+            for (long j = 0; j < nck && !met; ++j) {
+                const long a = t0 + j * ck, b = j + 1 < nck ? (a + ck < t1 ? a + ck : t1) : t1;
+                if (a >= b) break;
+                pll_run<U8, VEC, true>(ln, t, row, a, b, out + ch * ld_out, locked + ch * ld_out);
+                met = j + 1 < nck && same_state(cp[j], t);
+            }
+            if (met) t = endst[g];
             atomicAdd(recomputed, 1ull);
         }
     }
@@ -498,10 +519,11 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
 #define SDRGPU_PLL_SEG(V)                                                                          \
         hipLaunchKernelGGL((pll_seg_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
-                           spec.seg, spec.warm, nseg, spec.guess, spec.end);                        \
+                           spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.ck, spec.ckpt);    \
         hipLaunchKernelGGL((pll_fix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)nblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
-                           spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.recomputed)
+                           spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.recomputed,        \
+                           spec.ck, spec.ckpt)
         if (vec) { SDRGPU_PLL_SEG(true); } else { SDRGPU_PLL_SEG(false); }
 #undef SDRGPU_PLL_SEG
         return;
@@ -569,7 +591,8 @@ int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float*
                hipStream_t s) {
     if (n <= 0) return SDRGPU_OK;
     if (spec.seg > 0 && (spec.seg % kChunk || spec.warm % kChunk || !spec.guess || !spec.end ||
-                         !spec.recomputed))
+                         !spec.recomputed || spec.ck <= 0 || spec.ck % kChunk || spec.seg % spec.ck ||
+                         (spec.seg / spec.ck > 1 && !spec.ckpt)))
         return SDRGPU_ERR_INVALID;
     if (spec.seg > 0 && n > spec.seg)
         SDRGPU_HIP_TRY(hipMemsetAsync(spec.recomputed, 0, sizeof(unsigned long long), s));

@@ -34,6 +34,8 @@ struct PllSpec {
     PllChannelState* guess = nullptr;
     PllChannelState* end = nullptr;
     unsigned long long* recomputed = nullptr;  // segments pll_fix_kernel ran again (zeroed per block)
+    long ck = 0;                               // checkpoint interval inside a segment
+    PllChannelState* ckpt = nullptr;           // [segments][nch][seg / ck - 1] states at t0 + j ck
 };
 
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
