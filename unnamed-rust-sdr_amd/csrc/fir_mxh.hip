@@ -121,7 +121,10 @@ __device__ __forceinline__ float hi_f(unsigned u) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16));
 }
 
-// (a, b) already scaled: packed fp16 hi = rtz(x), lo = rtz(x - hi)
+// (a, b) already scaled: packed fp16 hi = rtz(x), lo = rtz(x - hi).  (Four
+// v_fma_mix{lo,hi}_f16 under a round-toward-zero f16 mode give the same bytes from 4 VALU
+// instead of 6 and run faster at steady state, but slower in the driver's window:
+// profiles/r05_fir_ring_ab.txt F.)
 __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
     hi = pk_rtz(a, b);
     lo = pk_rtz(a - lo_f(hi), b - hi_f(hi));
@@ -200,11 +203,12 @@ __device__ __forceinline__ float absmax4(float m, const float4& f) {
 }
 
 // window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float.  The
-// wave max uses DPP row reductions + 4 readlanes (non-negative floats order like their
-// bits): no LDS round trips on the per-tile critical path.
+// wave max uses DPP row reductions (each one v_max_u32 with a DPP source) + 4 readlanes
+// (non-negative floats order like their bits), and the exponent comes from the max's bits in
+// scalar ops: no LDS round trips and few vector instructions on the per-tile critical path.
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_umax(unsigned x) {
-    const unsigned y = (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false);
+    const unsigned y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
     return x > y ? x : y;
 }
 __device__ __forceinline__ int wave_scale(float m) {
@@ -216,7 +220,10 @@ __device__ __forceinline__ int wave_scale(float m) {
     const unsigned a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
     const unsigned c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
     const unsigned ab = a > b ? a : b, cd = c > d ? c : d;
-    int s = 15 - __builtin_amdgcn_frexp_expf(__uint_as_float(ab > cd ? ab : cd));
+    // 15 - frexp exponent = 141 - biased exponent for a normal max; a zero / subnormal max
+    // clamps to 126 as frexp's exponent would; inf / NaN (biased 255) keep frexp's 0 -> 15
+    const int e = (int)((ab > cd ? ab : cd) >> 23);
+    const int s = e == 255 ? 15 : 141 - e;
     return s < -126 ? -126 : (s > 126 ? 126 : s);
 }
 
