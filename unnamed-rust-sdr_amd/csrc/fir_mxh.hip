@@ -32,6 +32,7 @@
 // loop of the tile being computed.  4 x 2304 x 2 B = 18 KiB at NCH = 10 (was 20 KiB with
 // two separate window buffers).
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -100,7 +101,9 @@ struct MxhParams {
     const float* taps;
     float2* out;
     long ld_out;
-    long tpc, spc, seg_tiles, units;
+    long tpc, spc, seg_tiles, units;  // host-checked < 2^31 (tile cursors are 32-bit)
+    int ftiles;  // tiles wholly inside the input: tile t is fast iff t < ftiles (min(n_in / TI, 2^31 - 1))
+    int oblk;    // 256-output blocks wholly inside the output (min(n_out / 256, 2^31 - 1))
     int vec_out;
     int blocked;  // units in per-workgroup contiguous ranges, wave w takes units w, w+8, ...
 };
@@ -315,23 +318,27 @@ void fir_mxh_kernel(MxhParams p) {
     // computed and stored, k+1 staged, k+2 loading) advance together, so the raw-tile
     // prefetch crosses run boundaries; a run's first window re-reads the H samples before it
     // (issued one tile ahead, into the history registers).
+    // Cursor fields and every per-tile test are 32-bit (scalar compares; 64-bit ones are
+    // vector instructions on gfx950): tile t of a channel is "fast" (its window wholly inside
+    // the input) iff t < ftiles, and its outputs are whole 256-blocks iff t CS + j < oblk.
     struct Cur {
-        long u, t, ch, tu, nt;
+        int u, t, ch, tu, nt;
         bool ok;
     };
-    const long ust = p.blocked ? (long)kWaves : nwaves;
-    const long ub1 = p.blocked ? ((long)blockIdx.x + 1) * p.units / gridDim.x : p.units;
-    auto seek = [&](Cur& c, long u) {
+    const int units = (int)p.units, spc = (int)p.spc, segt = (int)p.seg_tiles, tpc = (int)p.tpc;
+    const int ust = p.blocked ? kWaves : (int)nwaves;
+    const int ub1 = p.blocked ? (int)(((long)blockIdx.x + 1) * p.units / gridDim.x) : units;
+    auto seek = [&](Cur& c, int u) {
         c.u = u;
         c.t = 0;
         c.ok = u < ub1;
-        if constexpr (D == 4 && !U8) {  // one stream (the headline): no 64-bit division per unit
-            c.ch = c.ok && p.spc < p.units ? u / p.spc : 0;
+        if constexpr (D == 4 && !U8) {  // one stream (the headline): no division per unit
+            c.ch = c.ok && spc < units ? u / spc : 0;
         } else {
-            c.ch = c.ok ? u / p.spc : 0;
+            c.ch = c.ok ? u / spc : 0;
         }
-        c.tu = (u - c.ch * p.spc) * p.seg_tiles;
-        c.nt = c.ok ? std::min(p.seg_tiles, p.tpc - c.tu) : 0;
+        c.tu = (u - c.ch * spc) * segt;
+        c.nt = c.ok ? std::min(segt, tpc - c.tu) : 0;
         if (c.ok && c.nt <= 0) c.ok = false;  // (units past a channel's last tile: none by construction)
     };
     auto adv = [&](Cur& c) {
@@ -340,7 +347,7 @@ void fir_mxh_kernel(MxhParams p) {
     };
     const long n_in = p.n_in;
     auto tile_j0 = [&](const Cur& c) { return (long)TI * (c.tu + c.t); };
-    auto tile_fast = [&](const Cur& c) { return (long)TI * (c.tu + c.t + 1) <= n_in; };
+    auto tile_fast = [&](const Cur& c) { return c.tu + c.t < p.ftiles; };
     auto fetch = [&](const Cur& c, long j) -> Raw {
         const float2* hist = p.hist + c.ch * (long)(K - 1);
         if constexpr (U8)
@@ -381,7 +388,8 @@ void fir_mxh_kernel(MxhParams p) {
     // the H samples before tile c (plain loads: the neighbouring wave streams them too)
     auto load_hist = [&](Raw (&dst)[NH], const Cur& c) {
         const long j = tile_j0(c) - H;
-        if (j >= 0 && j + H <= n_in) {
+        const int tile = c.tu + c.t;  // j >= 0 and j + H <= n_in (H <= TI)
+        if (tile >= 1 && tile <= p.ftiles) {
 #pragma unroll
             for (int k = 0; k < NH; ++k) dst[k] = ldx(c, j + 128 * k + 2 * lane, std::false_type());
         } else {
@@ -422,11 +430,18 @@ void fir_mxh_kernel(MxhParams p) {
         for (int i = 0; i < NH; ++i) hr[i] = nh[i];
     };
 
+    // byte offsets of the two line-complete output stores inside a tile's first 256-block
+    // (column set j adds 2048 j): the even lane of a pair writes its own 2 outputs and then
+    // the odd partner's first 2, the odd lane the even partner's last 2 and then its own
+    const bool ev = (v & 1) == 0;
+    const unsigned om = 8u * (16 * sv + 4 * g), omp = 8u * (16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g);
+    const unsigned ob1 = ev ? om : omp + 16, ob2 = ev ? omp : om + 16;
+
     // one raw tile in flight per wave (NG <= 8 groups of registers)
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
     static_assert(NG > NH, "an even window's last NH groups come from keep[]");
     Cur cm, st, ld;
-    seek(cm, p.blocked ? (long)blockIdx.x * p.units / gridDim.x + wv : wave);
+    seek(cm, p.blocked ? (int)((long)blockIdx.x * p.units / gridDim.x) + wv : (int)wave);
     if (cm.ok) {
         Raw nx[NG], hr[NH];
         load_hist(hr, cm);
@@ -553,23 +568,23 @@ void fir_mxh_kernel(MxhParams p) {
             }
             if (!fast2 && ld.ok) load_tile(nx, ld);
             const int so = -(s_cur + p.sh);
+            const int tile = cm.tu + cm.t;
             float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            const long m0 = (cm.tu + cm.t) * G::TO;
+            // the tile's output base is scalar; the lanes' byte offsets inside it are fixed
+            char* __restrict__ outt = reinterpret_cast<char*>(out + (long)tile * G::TO);
 #pragma unroll
             for (int j = 0; j < CS; ++j) {
-                const long m = m0 + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
                 float yr[4], yi[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
                     yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
                 }
-                if (p.vec_out && m0 + 256 * (j + 1) <= p.n_out) {
+                if (p.vec_out && tile * CS + j < p.oblk) {
                     // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
                     // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
                     // line) and the second those of the odd-v blocks (steady-state probe: 0.472
                     // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
-                    const bool ev = (v & 1) == 0;
                     const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
                     const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
                     f32x4 rx;
@@ -577,12 +592,10 @@ void fir_mxh_kernel(MxhParams p) {
                     for (int q = 0; q < 4; ++q)
                         rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
                             __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
-                    const long mp = m0 + 256 * j + 16 * (D == 4 ? sigma(v ^ 1) : (v ^ 1)) + 4 * g;
-                    f32x4* o4 = reinterpret_cast<f32x4*>(out + (ev ? m : mp + 2));
-                    f32x4* p4 = reinterpret_cast<f32x4*>(out + (ev ? mp : m + 2));
-                    __builtin_nontemporal_store(ev ? y0 : rx, o4);
-                    __builtin_nontemporal_store(ev ? rx : y1, p4);
+                    __builtin_nontemporal_store(ev ? y0 : rx, reinterpret_cast<f32x4*>(outt + (ob1 + 2048u * j)));
+                    __builtin_nontemporal_store(ev ? rx : y1, reinterpret_cast<f32x4*>(outt + (ob2 + 2048u * j)));
                 } else {
+                    const long m = (long)tile * G::TO + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
@@ -698,6 +711,11 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     p.spc = std::max(1L, ceil_div(p.tpc, p.seg_tiles));
     p.units = nch * p.spc;
     p.blocked = run > 0 && u8;
+    const long TI = 256L * cs * D;
+    p.ftiles = (int)std::min<long>(fp.n_in / TI, INT_MAX);
+    p.oblk = (int)std::min<long>(std::max(0L, fp.n_out) / 256, INT_MAX);
+    // 32-bit tile cursors (units, tiles per channel, unit / tile indices)
+    if (p.units >= INT_MAX - 8L * cus || p.tpc >= INT_MAX) return SDRGPU_ERR_UNSUPPORTED;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
 #define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
     hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
