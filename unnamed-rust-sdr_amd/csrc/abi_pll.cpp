@@ -108,7 +108,9 @@ struct sdrgpu_pll {
         sp->ck = ck;
         const size_t nck = (size_t)(sp->seg / ck - 1);
         const size_t nstate = (size_t)nseg * (size_t)dp.nch;
-        const size_t bytes = (2 + nck) * nstate * sizeof(PllChannelState) + 64;
+        // guess, end, end2, checkpoints, the counter (sdrgpu_pll_last_time_parallel reads it at
+        // state index (3 + nck) nstate), then the re-run marks
+        const size_t bytes = (3 + nck) * nstate * sizeof(PllChannelState) + nstate * sizeof(int) + 64;
         if (bytes > spec_buf.cap) {  // growing frees a buffer an earlier block may still use
             SDRGPU_HIP_TRY(hipStreamSynchronize(stream.cur));
             int st = spec_buf.ensure(bytes);
@@ -116,8 +118,10 @@ struct sdrgpu_pll {
         }
         sp->guess = static_cast<PllChannelState*>(spec_buf.ptr);
         sp->end = sp->guess + nseg * dp.nch;
-        sp->ckpt = nck ? sp->end + nstate : nullptr;
-        sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end + nstate + nck * nstate);
+        sp->end2 = sp->end + nstate;
+        sp->ckpt = nck ? sp->end2 + nstate : nullptr;
+        sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end2 + nstate + nck * nstate);
+        sp->rstop = reinterpret_cast<int*>(sp->recomputed + 8);
         last_nseg = nseg;
         last_nck = (long)nck;
         return SDRGPU_OK;
@@ -223,7 +227,7 @@ int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recompute
         unsigned long long r = 0;
         const auto* base = static_cast<const PllChannelState*>(h->spec_buf.ptr);
         SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
-        SDRGPU_HIP_TRY(hipMemcpy(&r, base + (2 + h->last_nck) * h->last_nseg * h->dp.nch, sizeof(r),
+        SDRGPU_HIP_TRY(hipMemcpy(&r, base + (3 + h->last_nck) * h->last_nseg * h->dp.nch, sizeof(r),
                                  hipMemcpyDeviceToHost));
         *recomputed = (long)r;
     }

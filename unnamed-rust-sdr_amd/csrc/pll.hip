@@ -301,13 +301,57 @@ __device__ __forceinline__ bool same_state(const PllChannelState& a, const PllCh
     return eq;
 }
 
+// Parallel re-run of the segments whose warm-up missed.  A segment's true start state is the
+// previous segment's end state, and pass 1's end state of the previous segment IS that state
+// whenever the previous segment ended on the true trajectory (its guess was right, or its
+// trajectory met the true one before its end -- the common case).  So every segment whose guess
+// differs from pass 1's end of its predecessor is re-run at once, one lane each, from that end
+// state, until it meets its own pass-1 trajectory at a checkpoint (rstop = +intervals run) or
+// to its end (rstop = -intervals, end state in end2).  pll_fix_kernel then only checks, per
+// channel and in order, that each re-run started from the true state; where one did not
+// (its predecessor's pass-1 end was not true), it recomputes that segment serially as before.
+template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
+__global__ __launch_bounds__(kPllBlock) void pll_refix_kernel(
+    PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
+    uint8_t* __restrict__ locked, long ld_out, long seg, long warm, long nseg,
+    const PllChannelState* __restrict__ guess, const PllChannelState* __restrict__ endst, long ck,
+    const PllChannelState* __restrict__ ckpt, int* __restrict__ rstop,
+    PllChannelState* __restrict__ end2) {
+    own_simd();
+    const long g = (long)blockIdx.x * kPllBlock + threadIdx.x;
+    if (g < p.nch || g >= p.nch * nseg) return;  // segment 0 starts from the carried state
+    const long ch = g % p.nch, sg = g / p.nch;
+    const long t0 = sg * seg, t1 = t0 + seg < n ? t0 + seg : n;
+    if (t0 <= warm || same_state(guess[g], endst[g - p.nch])) {
+        rstop[g] = 0;
+        return;
+    }
+    const PllLane<LID, OID, KID, MODE> ln(p);
+    const void* row = static_cast<const char*>(in_) + ch * ld_in * (U8 ? 2 : 8);
+    PllChannelState t = endst[g - p.nch];
+    const long nck = seg / ck;
+    const PllChannelState* __restrict__ cp = ckpt + g * (nck - 1);
+    int k = 0;
+    bool met = false;
+    for (long j = 0; j < nck && !met; ++j) {
+        const long a = t0 + j * ck, b = j + 1 < nck ? (a + ck < t1 ? a + ck : t1) : t1;
+        if (a >= b) break;
+        pll_run<U8, VEC, true>(ln, t, row, a, b, out + ch * ld_out, locked + ch * ld_out);
+        ++k;
+        met = j + 1 < nck && same_state(cp[j], t);
+    }
+    rstop[g] = met ? k : -k;
+    if (!met) end2[g] = t;
+}
+
 template <bool U8, int LID, int OID, int KID, int MODE, bool VEC>
 __global__ __launch_bounds__(kPllBlock) void pll_fix_kernel(
     PllDevParams p, const void* __restrict__ in_, long ld_in, long n, float* __restrict__ out,
     uint8_t* __restrict__ locked, long ld_out, PllChannelState* __restrict__ state, long seg,
     long warm, long nseg, const PllChannelState* __restrict__ guess,
     const PllChannelState* __restrict__ endst, unsigned long long* __restrict__ recomputed, long ck,
-    const PllChannelState* __restrict__ ckpt) {
+    const PllChannelState* __restrict__ ckpt, const int* __restrict__ rstop,
+    const PllChannelState* __restrict__ end2) {
     own_simd();
     const long ch = (long)blockIdx.x * kPllBlock + threadIdx.x;
     if (ch >= p.nch) return;
@@ -317,22 +361,34 @@ __global__ __launch_bounds__(kPllBlock) void pll_fix_kernel(
     for (long sg = 1; sg < nseg; ++sg) {
         const long t0 = sg * seg, t1 = t0 + seg < n ? t0 + seg : n;
         const long g = sg * p.nch + ch;
-        if (t0 <= warm || same_state(guess[g], t)) {
+        const bool hit = t0 <= warm || same_state(guess[g], t);
+        const int rs = rstop[g];
+        if (hit && rs == 0) {  // pass 1 ran from the true state and nothing overwrote it
             t = endst[g];
-        } else {  // the warm-up did not reach the true state: this segment again, from it, up
-                  // to the first checkpoint its trajectory meets (from there on it is exact)
-            const long nck = seg / ck;
-            const PllChannelState* __restrict__ cp = ckpt + g * (nck - 1);
-            bool met = false;
-            for (long j = 0; j < nck && !met; ++j) {
-                const long a = t0 + j * ck, b = j + 1 < nck ? (a + ck < t1 ? a + ck : t1) : t1;
-                if (a >= b) break;
-                pll_run<U8, VEC, true>(ln, t, row, a, b, out + ch * ld_out, locked + ch * ld_out);
-                met = j + 1 < nck && same_state(cp[j], t);
-            }
-            if (met) t = endst[g];
-            atomicAdd(recomputed, 1ull);
+            continue;
         }
+        if (!hit) {
+            atomicAdd(recomputed, 1ull);
+            if (rs != 0 && same_state(endst[g - p.nch], t)) {  // re-run from the true state: exact
+                t = rs > 0 ? endst[g] : end2[g];
+                continue;
+            }
+        }
+        // the warm-up did not reach the true state and no re-run started from it, or a re-run
+        // from a wrong state (its predecessor's pass-1 end) overwrote outputs of a segment whose
+        // guess was right: this segment again from the true state, up to the first checkpoint
+        // its trajectory meets (from there on it is exact) and at least over the overwritten
+        // intervals
+        const long nck = seg / ck, over = rs < 0 ? -rs : rs;
+        const PllChannelState* __restrict__ cp = ckpt + g * (nck - 1);
+        bool met = false;
+        for (long j = 0; j < nck && !(met && j >= over); ++j) {
+            const long a = t0 + j * ck, b = j + 1 < nck ? (a + ck < t1 ? a + ck : t1) : t1;
+            if (a >= b) break;
+            pll_run<U8, VEC, true>(ln, t, row, a, b, out + ch * ld_out, locked + ch * ld_out);
+            met = j + 1 < nck && same_state(cp[j], t);
+        }
+        if (met) t = endst[g];
     }
     state[ch] = t;
 }
@@ -520,10 +576,14 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
         hipLaunchKernelGGL((pll_seg_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
                            spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.ck, spec.ckpt);    \
+        hipLaunchKernelGGL((pll_refix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),    \
+                           dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, spec.seg,   \
+                           spec.warm, nseg, spec.guess, spec.end, spec.ck, spec.ckpt, spec.rstop,   \
+                           spec.end2);                                                              \
         hipLaunchKernelGGL((pll_fix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)nblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
                            spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.recomputed,        \
-                           spec.ck, spec.ckpt)
+                           spec.ck, spec.ckpt, spec.rstop, spec.end2)
         if (vec) { SDRGPU_PLL_SEG(true); } else { SDRGPU_PLL_SEG(false); }
 #undef SDRGPU_PLL_SEG
         return;
@@ -592,7 +652,7 @@ int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float*
     if (n <= 0) return SDRGPU_OK;
     if (spec.seg > 0 && (spec.seg % kChunk || spec.warm % kChunk || !spec.guess || !spec.end ||
                          !spec.recomputed || spec.ck <= 0 || spec.ck % kChunk || spec.seg % spec.ck ||
-                         (spec.seg / spec.ck > 1 && !spec.ckpt)))
+                         (spec.seg / spec.ck > 1 && !spec.ckpt) || !spec.rstop || !spec.end2))
         return SDRGPU_ERR_INVALID;
     if (spec.seg > 0 && n > spec.seg)
         SDRGPU_HIP_TRY(hipMemsetAsync(spec.recomputed, 0, sizeof(unsigned long long), s));

@@ -36,6 +36,11 @@ struct PllSpec {
     unsigned long long* recomputed = nullptr;  // segments pll_fix_kernel ran again (zeroed per block)
     long ck = 0;                               // checkpoint interval inside a segment
     PllChannelState* ckpt = nullptr;           // [segments][nch][seg / ck - 1] states at t0 + j ck
+    // parallel re-run (pll_refix_kernel): per segment, +k = re-run from the previous segment's
+    // end met this trajectory after k intervals, -k = ran k intervals without meeting it (end
+    // state in end2), 0 = not re-run
+    int* rstop = nullptr;
+    PllChannelState* end2 = nullptr;
 };
 
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,
