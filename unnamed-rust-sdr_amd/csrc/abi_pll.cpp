@@ -78,17 +78,21 @@ struct sdrgpu_pll {
     long last_nck = 0;   // and the checkpoints per segment it kept
 
     // The plan for a block of n samples.  Auto: enough segments per channel to give every SIMD
-    // one wave (64 channel-segments each), none shorter than the warm-up (16 Ki samples: every
-    // configs[3] channel's state had converged within 12.2 Ki).
+    // one wave (64 channel-segments each), none shorter than 16 Ki samples (a segment whose
+    // re-run from the true state has not met its pass-1 trajectory by its end hands a wrong
+    // start to its successor; every configs[3] channel's state had converged within 12.2 Ki,
+    // DESIGN.md 3.6), warm-up 4 Ki (with the parallel re-run pass, 8 to 16 Ki of warm-up all
+    // come to 11.4-13.2 ms at configs[3]: profiles/r05_pll_refix_sweep.txt).
+    static constexpr long kMinSeg = 16384, kWarm = 4096;
     void plan(long n, long* seg, long* warm) const {
         *seg = 0;
-        *warm = tp_warm > 0 ? (tp_warm + 7) / 8 * 8 : 16384;
+        *warm = tp_warm > 0 ? (tp_warm + 7) / 8 * 8 : kWarm;
         if (tp_seg < 0 || n <= 0) return;
         long sg;
         if (tp_seg > 0) {
             sg = (tp_seg + 7) / 8 * 8;
         } else {
-            const long by_lanes = 64 * simds / dp.nch, by_len = n / *warm;
+            const long by_lanes = 64 * simds / dp.nch, by_len = n / kMinSeg;
             const long nseg = by_lanes < by_len ? by_lanes : by_len;
             if (nseg < 2) return;
             sg = ((n + nseg - 1) / nseg + 7) / 8 * 8;
