@@ -45,7 +45,7 @@ struct FirOsPlan;
 int fir_os_supported(int sample_kind, int tap_kind, int K, int D);
 
 // LDS-staged direct form on a per-tile scaled two-way fp16 split, two waves per SIMD
-// (fir_mxh.hip): D = 4 (K <= 257, also u8 input) and D = 1 (K <= 273).  tap_scale_exp:
+// (fir_mxh.hip): D = 4 (K <= 257, also u8 input), D = 2 (K <= 257) and D = 1 (K <= 273).  tap_scale_exp:
 // taps are multiplied by 2^tap_scale_exp before the split.  d_dummy: fir_mxh_dummy_bytes()
 // of zeroed device memory (target of the clamped prefetches at a stream's end).
 size_t fir_mxh_dummy_bytes();
