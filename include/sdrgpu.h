@@ -350,6 +350,19 @@ int sdrgpu_biquad_process(sdrgpu_biquad* h, const void* in, size_t ld_in, size_t
                           size_t ld_out);
 int sdrgpu_biquad_process_dev(sdrgpu_biquad* h, const void* d_in, size_t ld_in, size_t n,
                               void* d_out, size_t ld_out);
+/* Time-parallel blocks (no reference counterpart: Biquad::apply is serial, biquad.rs:42-56;
+ * outputs stay identical to it).  A channel's block is cut into segments of `seg` samples
+ * that run at once, each after `warm` samples of warm-up from zero output history, verified
+ * bit for bit against the true state and recomputed where they differ.  seg = warm = 0:
+ * automatic (warm-up from the filter's slower pole, enough segments to fill the device, none
+ * for Identity, an unstable design or a block that gives fewer than two); seg < 0: always
+ * one serial pass.  Mirrors sdrgpu_pll_set_time_parallel. */
+int sdrgpu_biquad_set_time_parallel(sdrgpu_biquad* h, long seg, long warm);
+/* the (segment, warm-up) a block of n samples per channel would use (segment 0: serial) */
+int sdrgpu_biquad_time_parallel_plan(const sdrgpu_biquad* h, size_t n, long* seg, long* warm);
+/* segments per channel of the most recent block (0: serial) and how many missed their guess
+ * (synchronizes the handle's stream) */
+int sdrgpu_biquad_last_time_parallel(sdrgpu_biquad* h, long* segments, long* recomputed);
 int sdrgpu_biquad_sync(sdrgpu_biquad* h);
 int sdrgpu_biquad_reset(sdrgpu_biquad* h);
 int sdrgpu_biquad_clone(const sdrgpu_biquad* h, sdrgpu_biquad** out);

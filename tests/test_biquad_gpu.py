@@ -57,3 +57,88 @@ def test_biquad_state_carry_reset_clone(sdr, oracle):
     v = one.apply(np.float32(1.0))
     c = sdr.filter.BiquadD.Lr(75e-6).to_c()
     assert v == oracle.biquad_run(c.kind, c.freq, c.q, RATE, np.array([1.0], np.float32))[0]
+
+
+TP_CASES = [("LowPass", (20000.0, 0.7), 1.8e6), ("BandPass", (19000.0, 5.0), 1.8e6),
+            ("Lr", (1.0 / 75e-6,), 144000.0), ("LowPass", (200.0, 0.7), 144000.0)]  # main.rs:52,57
+
+
+def _signal(rng, sk, nch, n):
+    if sk:
+        return (rng.standard_normal((nch, n)) + 1j * rng.standard_normal((nch, n))).astype(np.complex64)
+    return rng.standard_normal((nch, n)).astype(np.float32)
+
+
+@pytest.mark.parametrize("sk", [0, 1], ids=["f32", "c64"])
+@pytest.mark.parametrize("name,args,rate", TP_CASES, ids=["lp20k", "bp19k", "deemph", "lp200hz"])
+def test_biquad_time_parallel_auto_bit_exact(sdr, oracle, name, args, rate, sk):
+    """A few long streams (the de-emphasis / pilot-filter shape of src/main.rs:52-60, and the
+    PLL's lock filter at 1.8 Msps) through the automatic time-parallel plan: segments run at
+    once after a warm-up sized from the design's slower pole, verified bit for bit and
+    recomputed where they miss -- outputs array_equal to the oracle's serial Biquad::apply,
+    over two calls (state carried), and to the handle's own serial pass."""
+    rng = np.random.default_rng(90 + sk + int(rate) % 7)
+    nch, n, cut = 3, 1200000, 800000
+    d = getattr(sdr.filter.BiquadD, name)(*args)
+    bq = d.design(rate, sample_kind=sk, nch=nch)
+    seg, warm = bq.time_parallel_plan(cut)
+    assert seg > 0 and warm >= 64 and seg >= 4 * warm, (seg, warm)
+    x = _signal(rng, sk, nch, n)
+    y1 = bq.process(x[:, :cut])
+    segs, rec = bq.last_time_parallel()
+    assert segs >= 2 and 0 <= rec <= nch * (segs - 1)
+    y = np.concatenate([y1, bq.process(x[:, cut:])], axis=1)
+    c = d.to_c()
+    for ch in range(nch):
+        np.testing.assert_array_equal(y[ch], oracle.biquad_run(c.kind, c.freq, c.q, rate, x[ch]),
+                                      err_msg=f"{name} ch {ch}")
+    serial = d.design(rate, sample_kind=sk, nch=nch)
+    serial.set_time_parallel(-1)
+    assert serial.time_parallel_plan(n)[0] == 0
+    np.testing.assert_array_equal(serial.process(x), y)
+
+
+@pytest.mark.parametrize("seg,warm", [(4096, 8), (1000, 200), (8192, 100000), (2048, 1024)],
+                         ids=["mostly-recomputed", "ragged", "warm-reaches-start", "converging"])
+def test_biquad_time_parallel_forced(sdr, oracle, seg, warm):
+    """Forced segment / warm-up lengths on 70 complex channels: a warm-up so short that nearly
+    every segment misses its guess (the re-run and serial repair paths), a segment length that
+    leaves a ragged last segment, a warm-up reaching back to the block start (exact guesses)
+    and a converging one; array_equal to the oracle, state carried into a second block."""
+    rng = np.random.default_rng(seg + warm)
+    nch, n = 70, 30011
+    d = sdr.filter.BiquadD.LowPass(20000.0, 0.7)
+    bq = d.design(RATE, sample_kind=1, nch=nch)
+    bq.set_time_parallel(seg, warm)
+    assert bq.time_parallel_plan(20000) == ((seg + 7) // 8 * 8, warm)
+    x = _signal(rng, 1, nch, n)
+    y1 = bq.process(x[:, :20000])
+    segs, rec = bq.last_time_parallel()
+    assert segs == -(-20000 // ((seg + 7) // 8 * 8))
+    if warm >= 20000:
+        assert rec == 0
+    if warm == 8:
+        assert rec > nch
+    y = np.concatenate([y1, bq.process(x[:, 20000:])], axis=1)
+    c = d.to_c()
+    for ch in (0, 1, 33, 64, nch - 1):
+        np.testing.assert_array_equal(y[ch], oracle.biquad_run(c.kind, c.freq, c.q, RATE, x[ch]),
+                                      err_msg=f"ch {ch}")
+
+
+def test_biquad_time_parallel_not_for_identity_integrator_or_many_channels(sdr):
+    """Identity has no recurrence, Lr(75e-6) at 144 kHz rounds its pole to exactly 1.0 in f32
+    (an integrator: two trajectories never meet), the pilot's LowPass(20 Hz) at 144 kHz has its
+    poles within 0.07 % of the unit circle, and 65536 channels already fill the device: serial
+    plans (an explicit set_time_parallel still applies)."""
+    f = sdr.filter
+    ident = f.Identity.design(RATE, sample_kind=0, nch=1)
+    assert ident.time_parallel_plan(1 << 20)[0] == 0
+    integ = f.BiquadD.Lr(75e-6).design(144000.0, sample_kind=0, nch=1)
+    assert integ.coefs()[3] == 1.0 and integ.time_parallel_plan(1 << 20)[0] == 0
+    pilot = f.BiquadD.LowPass(20.0, 0.7).design(144000.0, sample_kind=0, nch=1)
+    assert pilot.time_parallel_plan(1 << 24) == (0, 0)
+    pilot.set_time_parallel(1 << 20, 1 << 16)
+    assert pilot.time_parallel_plan(1 << 24) == (1 << 20, 1 << 16)
+    many = f.BiquadD.LowPass(20000.0, 0.7).design(RATE, sample_kind=0, nch=65536)
+    assert many.time_parallel_plan(1 << 16)[0] == 0

@@ -186,6 +186,9 @@ SIGNATURES = [
     ("sdrgpu_biquad_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_biquad_process", c_int, [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t]),
     ("sdrgpu_biquad_process_dev", c_int, [_H, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t]),
+    ("sdrgpu_biquad_set_time_parallel", c_int, [_H, c_long, c_long]),
+    ("sdrgpu_biquad_time_parallel_plan", c_int, [_H, c_size_t, POINTER(c_long), POINTER(c_long)]),
+    ("sdrgpu_biquad_last_time_parallel", c_int, [_H, POINTER(c_long), POINTER(c_long)]),
     ("sdrgpu_biquad_sync", c_int, [_H]),
     ("sdrgpu_biquad_reset", c_int, [_H]),
     ("sdrgpu_biquad_clone", c_int, [_H, _PH]),

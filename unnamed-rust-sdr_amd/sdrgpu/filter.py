@@ -418,6 +418,23 @@ class Biquad:
         check(lib().sdrgpu_biquad_process_dev(self._h, d_in, ld_in, n, d_out, ld_out),
               "sdrgpu_biquad_process_dev")
 
+    def set_time_parallel(self, seg: int = 0, warm: int = 0):
+        """Segments of `seg` samples with `warm` samples of warm-up (0, 0: automatic; seg < 0:
+        always serial); outputs identical to the serial recurrence."""
+        check(lib().sdrgpu_biquad_set_time_parallel(self._h, seg, warm), "set_time_parallel")
+
+    def time_parallel_plan(self, n: int):
+        s, w = ctypes.c_long(), ctypes.c_long()
+        check(lib().sdrgpu_biquad_time_parallel_plan(self._h, n, ctypes.byref(s), ctypes.byref(w)),
+              "time_parallel_plan")
+        return s.value, w.value
+
+    def last_time_parallel(self):
+        s, r = ctypes.c_long(), ctypes.c_long()
+        check(lib().sdrgpu_biquad_last_time_parallel(self._h, ctypes.byref(s), ctypes.byref(r)),
+              "last_time_parallel")
+        return s.value, r.value
+
     def sync(self):
         check(lib().sdrgpu_biquad_sync(self._h), "sdrgpu_biquad_sync")
 
