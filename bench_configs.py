@@ -40,7 +40,7 @@ HBM_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex", "all"])
+    ap.add_argument("--config", default="all", choices=["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex", "fm", "all"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c3-log2n", type=int, default=28)
@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--c5-nch", type=int, default=8192)
     ap.add_argument("--c5-log2n", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--fm-seconds", type=float, default=10.0, help="seconds of air through the fm chain")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="timing-only ablation builds: skip the c3 / c5 spot checks")
     ap.add_argument("--gpus", type=int, default=1,
@@ -543,6 +544,65 @@ def bench_src(args):
     return lines
 
 
+# ------------------------------------------------------------------------------ fm
+def fm_stereo_u8(n, seed=0, rate=1.8e6):
+    """A synthetic FM stereo broadcast as rtl_tcp u8 I/Q (the generator of
+    tests/test_fm_chain_gpu.py): (L + R) + 0.1 pilot + (L - R) at 38 kHz DSB, 75 kHz deviation."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / rate
+    left = 0.4 * np.sin(2 * np.pi * 440.0 * t)
+    right = 0.4 * np.sin(2 * np.pi * 1250.0 * t + 0.3)
+    comp = (0.45 * (left + right) + 0.1 * np.cos(2 * np.pi * 19000.0 * t)
+            + 0.45 * (left - right) * np.cos(2 * np.pi * 38000.0 * t))
+    iq = np.exp(1j * 2 * np.pi * 75000.0 * np.cumsum(comp) / rate) * 0.8
+    iq = iq + 0.02 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    raw = np.empty(2 * n, np.uint8)
+    raw[0::2] = np.clip(np.round(iq.real * 127.5 + 127.5), 0, 255).astype(np.uint8)
+    raw[1::2] = np.clip(np.round(iq.imag * 127.5 + 127.5), 0, 255).astype(np.uint8)
+    return raw
+
+
+def bench_fm(args):
+    """src/main.rs:33-81 end to end (sdrgpu.fm.receiver: PLL discriminator on the rtl_tcp bytes,
+    SincFastest to 144 kHz, pilot-PLL stereo difference, SincBestQuality to 48 kHz, de-emphasis)
+    over `--fm-seconds` of synthetic air in the reference's 0.1 s blocks (block(0.1), main.rs:47):
+    seconds of air per second of wall time, host bytes in and audio out included (the chain's
+    blocks come from and go to host memory, as main.rs's socket and WAV writer do).  The CPU
+    baseline is the oracle's restatement of the same chain (tests/test_fm_chain_gpu.py's
+    composition) on 1 s of air."""
+    from sdrgpu import _lib, fm
+    from sdrgpu.signal import from_array
+    rate = fm.RATE
+    n = int(rate * args.fm_seconds)
+    raw = fm_stereo_u8(n)
+    blk = int(rate * 0.1)
+    warm = from_array(rate, raw[:2 * blk * 5], block=blk, sample_kind=_lib.CU8)
+    list(fm.receiver(warm).blocks())
+    rtl = from_array(rate, raw, block=blk, sample_kind=_lib.CU8)
+    t0 = time.perf_counter()
+    out = np.concatenate(list(fm.receiver(rtl).blocks()), axis=0)
+    el = time.perf_counter() - t0
+    res = {"config": "fm: src/main.rs FM stereo receiver chain, 1 station, u8 I/Q at 1.8 Msps in 0.1 s blocks",
+           "metric": "seconds of air per second (real-time factor)",
+           "value": round(args.fm_seconds / el, 1), "air_seconds": args.fm_seconds,
+           "wall_s": round(el, 3), "audio_frames": int(out.shape[0]),
+           "input_Msps": round(n / el / 1e6, 1)}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import pyoracle
+        from bench import host_info
+        from test_fm_chain_gpu import oracle_chain
+        cs = min(1.0, args.fm_seconds)
+        t0 = time.perf_counter()
+        oracle_chain(pyoracle, raw[:2 * int(rate * cs)], fm)
+        ce = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(cs / ce, 2), "unit": "seconds of air per second",
+                               "cores": 1, "kind": "port", "host": host_info(),
+                               "sample": f"{cs:.1f} s of air through the oracle's chain, {ce:.1f} s"}
+    return res
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -550,10 +610,11 @@ def main():
             sys.exit("--gpus > 1 applies to --config c5 only")
         from bench import launch_ranks
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
-    todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex"] if args.config == "all" else [args.config]
+    todo = ["c1", "c3", "c4", "c5", "c2u8", "c2host", "c2pinned", "src", "ex", "fm"] if args.config == "all" else [args.config]
     for c in todo:
         r = {"c1": bench_c1, "c3": bench_c3, "c4": bench_c4, "c5": bench_c5, "c2u8": bench_c2u8,
-             "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src, "ex": bench_ex}[c](args)
+             "c2host": bench_c2host, "c2pinned": bench_c2pinned, "src": bench_src, "ex": bench_ex,
+             "fm": bench_fm}[c](args)
         for line in (r if isinstance(r, list) else [r]):
             if line is not None:
                 print(json.dumps(line), flush=True)

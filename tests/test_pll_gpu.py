@@ -383,18 +383,18 @@ def test_pll_time_parallel_other_designs_and_u8(sdr, oracle):
 def test_pll_time_parallel_auto_plan_configs3(sdr, oracle):
     """The automatic plan at configs[3]'s shape (1024 channels x 2^20: 64 segments of 16 Ki,
     4 Ki of warm-up, one wave per SIMD), and a 1024-channel block of 2^17 samples through it
-    (auto plan: 8 segments) array_equal to the oracle on 8 channels."""
+    (auto plan: 32 segments of 4 Ki) array_equal to the oracle on 8 channels."""
     nch = 1024
     pll = main_rs_design(sdr).design(RATE, nch=nch)
     assert pll.time_parallel_plan(1 << 20) == (16384, 4096)
-    assert pll.time_parallel_plan(16384) == (0, 4096)      # one segment: serial
+    assert pll.time_parallel_plan(8191) == (0, 4096)       # under two segments: serial
     rng = np.random.default_rng(1024)
     n = 1 << 17
     chans = [0, 63, 64, 511, 777, 1000, 1022, 1023]
     x = np.empty((nch, n), np.complex64)
     x[:] = fm_channels(rng, 1, n)[0]                           # one waveform everywhere ...
     x[chans] = fm_channels(rng, len(chans), n)                 # ... and 8 different channels
-    assert pll.time_parallel_plan(n) == (16384, 4096)
+    assert pll.time_parallel_plan(n) == (4096, 4096)
     out, lk = pll.process(x)
     ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), np.ascontiguousarray(x[chans]), nthreads=8)
     check(out[chans], lk[chans], ref_out, ref_lk, "configs[3] auto plan")

@@ -78,12 +78,14 @@ struct sdrgpu_pll {
     long last_nck = 0;   // and the checkpoints per segment it kept
 
     // The plan for a block of n samples.  Auto: enough segments per channel to give every SIMD
-    // one wave (64 channel-segments each), none shorter than 16 Ki samples (a segment whose
-    // re-run from the true state has not met its pass-1 trajectory by its end hands a wrong
-    // start to its successor; every configs[3] channel's state had converged within 12.2 Ki,
-    // DESIGN.md 3.6), warm-up 4 Ki (with the parallel re-run pass, 8 to 16 Ki of warm-up all
-    // come to 11.4-13.2 ms at configs[3]: profiles/r05_pll_refix_sweep.txt).
-    static constexpr long kMinSeg = 16384, kWarm = 4096;
+    // one wave (64 channel-segments each), none shorter than 4 Ki samples, warm-up 4 Ki.  A
+    // segment's pass-1 trajectory has had warm-up + segment samples to meet the true one before
+    // its successor's re-run starts from its end; every configs[3] channel's state had converged
+    // within 12.2 Ki.  Measured: configs[3] (64 segments of 16 Ki either way)
+    // 8 Ki to 16 Ki of warm-up all at 11.4-13.2 ms (profiles/r05_pll_refix_sweep.txt); one
+    // 1.8 Msps stream in main.rs's 0.1 s blocks, 4 Ki segments 6.2 ms per block against 9.7 at
+    // the 16 Ki minimum and 53 serially, 2 Ki segments 20 ms (profiles/r05_pll_tp_single.txt).
+    static constexpr long kMinSeg = 4096, kWarm = 4096;
     void plan(long n, long* seg, long* warm) const {
         *seg = 0;
         *warm = tp_warm > 0 ? (tp_warm + 7) / 8 * 8 : kWarm;
