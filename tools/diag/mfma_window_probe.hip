@@ -6,6 +6,7 @@
 // workgroup per CU, sized to ~0.5 ms at full clock:
 //   f16:  v_mfma_f32_16x16x32_f16   (the c64 FIR's instruction)
 //   i8:   v_mfma_i32_16x16x64_i8    (the u8 FIR's; twice the K per instruction)
+//   f16k16: v_mfma_f32_16x16x16_f16 (half the K of the f16 arm: is it half the cycles?)
 // argv[1] = arm, argv[2] = iterations per wave.  Prints per-launch times: 1 s idle, then 25
 // launches (the driver's 5 warmup + 20 timed), then 200 back to back.
 #include <hip/hip_runtime.h>
@@ -53,6 +54,14 @@ __global__ __launch_bounds__(512) void probe(long iters, float* __restrict__ sin
             __builtin_memcpy(&B, m, 16);
 #pragma unroll
             for (int j = 0; j < 8; ++j) cf[j & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, cf[j & 3], 0, 0, 0);
+        } else if constexpr (ARM == 2) {
+            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+            unsigned m[2] = {nb[0] & 0x3bff3bffu, nb[1] & 0x3bff3bffu};
+            f16x4 A, B;
+            __builtin_memcpy(&A, a, 8);
+            __builtin_memcpy(&B, m, 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cf[j & 3] = __builtin_amdgcn_mfma_f32_16x16x16f16(A, B, cf[j & 3], 0, 0, 0);
         } else {
             typedef int i32x4t __attribute__((ext_vector_type(4)));
             i32x4t A, B;
@@ -77,7 +86,7 @@ __global__ __launch_bounds__(512) void probe(long iters, float* __restrict__ sin
     } while (0)
 
 int main(int argc, char** argv) {
-    const int arm = argc > 1 ? (strcmp(argv[1], "i8") == 0) : 0;
+    const int arm = argc > 1 ? (strcmp(argv[1], "i8") == 0 ? 1 : strcmp(argv[1], "f16k16") == 0 ? 2 : 0) : 0;
     const long iters = argc > 2 ? atol(argv[2]) : 2000;
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -89,7 +98,8 @@ int main(int argc, char** argv) {
     std::vector<hipEvent_t> ev(nl + 1);
     for (auto& e : ev) CK(hipEventCreate(&e));
     auto go = [&]() {
-        if (arm) hipLaunchKernelGGL(probe<1>, dim3(cus), dim3(512), 0, st, iters, sink);
+        if (arm == 1) hipLaunchKernelGGL(probe<1>, dim3(cus), dim3(512), 0, st, iters, sink);
+        else if (arm == 2) hipLaunchKernelGGL(probe<2>, dim3(cus), dim3(512), 0, st, iters, sink);
         else hipLaunchKernelGGL(probe<0>, dim3(cus), dim3(512), 0, st, iters, sink);
     };
     go();  // load the code object
@@ -107,7 +117,7 @@ int main(int argc, char** argv) {
     for (int i = 5; i < 25; ++i) w += ms[i];
     for (int i = 25; i < nl; ++i) l += ms[i];
     printf("{\"arm\": \"%s\", \"iters\": %ld, \"driver_window_ms\": %.4f, \"steady_ms\": %.4f, \"first25\": [",
-           arm ? "i8" : "f16", iters, w / 20, l / 200);
+           arm == 1 ? "i8" : arm == 2 ? "f16k16" : "f16", iters, w / 20, l / 200);
     for (int i = 0; i < 25; ++i) printf("%s%.4f", i ? ", " : "", ms[i]);
     printf("]}\n");
     return 0;
