@@ -343,6 +343,13 @@ impl<A: GpuSample> GpuBiquad<A> {
                                        output.as_mut_ptr() as *mut _, n)
         })
     }
+
+    /// Long blocks of few channels run as verified speculative segments by default (outputs
+    /// identical to Biquad::apply's serial recurrence); `seg < 0` forces one serial pass,
+    /// `(0, 0)` restores the automatic plan.
+    pub fn set_time_parallel(&mut self, seg: i64, warm: i64) -> Result<()> {
+        check(unsafe { sys::sdrgpu_biquad_set_time_parallel(self.h, seg as _, warm as _) })
+    }
 }
 
 impl<A: GpuSample> Filter<A> for GpuBiquad<A> {
@@ -471,6 +478,13 @@ impl GpuPll {
 
     pub fn reset(&mut self) -> Result<()> {
         check(unsafe { sys::sdrgpu_pll_reset(self.h) })
+    }
+
+    /// Long blocks run as verified speculative segments by default (outputs identical to
+    /// Pll::apply's serial recurrence); `seg < 0` forces one serial pass, `(0, 0)` restores
+    /// the automatic plan.
+    pub fn set_time_parallel(&mut self, seg: i64, warm: i64) -> Result<()> {
+        check(unsafe { sys::sdrgpu_pll_set_time_parallel(self.h, seg as _, warm as _) })
     }
 }
 
