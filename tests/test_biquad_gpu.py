@@ -142,3 +142,32 @@ def test_biquad_time_parallel_not_for_identity_integrator_or_many_channels(sdr):
     assert pilot.time_parallel_plan(1 << 24) == (1 << 20, 1 << 16)
     many = f.BiquadD.LowPass(20000.0, 0.7).design(RATE, sample_kind=0, nch=65536)
     assert many.time_parallel_plan(1 << 16)[0] == 0
+
+
+def test_biquad_time_parallel_strided_device_rows(sdr, oracle):
+    """Time-parallel blocks on device rows with leading dimensions larger than the block (ld_in
+    = n + 37, ld_out = n + 5, as a caller's channel-major buffers give them), c64 and f32,
+    two blocks with the state carried: array_equal to the oracle."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(77)
+    d = sdr.filter.BiquadD.LowPass(20000.0, 0.7)
+    for sk, dt in ((1, np.complex64), (0, np.float32)):
+        nch, n = 2, 300000
+        bq = d.design(RATE, sample_kind=sk, nch=nch)
+        assert bq.time_parallel_plan(n // 2)[0] > 0
+        x = _signal(rng, sk, nch, n)
+        ldi, ldo = n // 2 + 37, n // 2 + 5
+        halves = []
+        for h in range(2):
+            xi = np.zeros((nch, ldi), dt)
+            xi[:, :n // 2] = x[:, h * (n // 2):(h + 1) * (n // 2)]
+            dx = DeviceBuffer.from_numpy(xi)
+            dy = DeviceBuffer.empty(nch * ldo, dt)
+            bq.process_dev(dx.ptr, ldi, n // 2, dy.ptr, ldo)
+            bq.sync()
+            assert bq.last_time_parallel()[0] >= 2
+            halves.append(dy.download(nch * ldo, dt).reshape(nch, ldo)[:, :n // 2])
+        y = np.concatenate(halves, axis=1)
+        c = d.to_c()
+        for ch in range(nch):
+            np.testing.assert_array_equal(y[ch], oracle.biquad_run(c.kind, c.freq, c.q, RATE, x[ch]))
