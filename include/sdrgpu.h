@@ -293,10 +293,11 @@ int sdrgpu_pll_set_output_mode(sdrgpu_pll* h, int mode);
 int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind);
 /* Time-parallel blocks (no reference counterpart; results are the serial PLL's bit for bit):
  * each channel's block is cut into segments of `seg` samples that run concurrently, each after
- * `warm` samples of warm-up from the design state; a segment whose warm-up did not reach the
- * true state exactly is recomputed from it.  seg = 0: automatic (enough
- * segments to give every SIMD one wave, none shorter than the warm-up), seg < 0: always one
- * serial pass; warm = 0: 16384.  Lengths round up to multiples of 8. */
+ * `warm` samples of warm-up from the design state; segments whose warm-up did not reach the
+ * true state exactly are re-run in parallel from their predecessor's end state and, where that
+ * was not true either, recomputed from the true state.  seg = 0: automatic
+ * (enough segments to give every SIMD one wave, none shorter than 4096 samples), seg < 0:
+ * always one serial pass; warm = 0: 4096.  Lengths round up to multiples of 8. */
 int sdrgpu_pll_set_time_parallel(sdrgpu_pll* h, long seg, long warm);
 /* The segment length (0 = one serial pass) and warm-up a block of n samples would use. */
 int sdrgpu_pll_time_parallel_plan(const sdrgpu_pll* h, size_t n, long* seg, long* warm);
