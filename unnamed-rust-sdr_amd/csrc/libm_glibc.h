@@ -448,7 +448,8 @@ SDR_LIBM_FN float sdr_atan2f_bfx(float y, float x) {
      * half an ulp of pi_lo (2^-48), so za - pi_lo rounds to exactly 0 - pi_lo. */
     const float zq = (hx < 0) ? pi - (za - pi_lo) : za;
     const float gen = sdr_asfloat((sdr_asuint(zq) & 0x7fffffffu) | ((uint32_t)hy & 0x80000000u));
-    /* special cases, reference order (later checks apply only where earlier ones did not) */    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
+    /* special cases, reference order (later checks apply only where earlier ones did not) */
+    const float by_m_pi = (m <= 1) ? y : (m == 2 ? pi + tiny : -pi - tiny);          /* y == 0 */
     const float half = (hy < 0) ? -pi_o_2 - tiny : pi_o_2 + tiny;                  /* x == 0, y = inf */
     const float infinf = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny
                        : m == 2 ? (float)3.0 * pi_o_4 + tiny : (float)-3.0 * pi_o_4 - tiny;
