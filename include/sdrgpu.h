@@ -297,7 +297,10 @@ int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind);
  * true state exactly are re-run in parallel from their predecessor's end state and, where that
  * was not true either, recomputed from the true state.  seg = 0: automatic
  * (enough segments to give every SIMD one wave, none shorter than 4096 samples), seg < 0:
- * always one serial pass; warm = 0: 4096.  Lengths round up to multiples of 8. */
+ * always one serial pass; warm = 0: 4096.  Lengths round up to multiples of 8.  A
+ * sdrgpu_pll_process_dev call whose output or lock range overlaps its input range (in place)
+ * runs one serial pass whatever the plan (the segment kernels re-read inputs after outputs are
+ * stored). */
 int sdrgpu_pll_set_time_parallel(sdrgpu_pll* h, long seg, long warm);
 /* The segment length (0 = one serial pass) and warm-up a block of n samples would use. */
 int sdrgpu_pll_time_parallel_plan(const sdrgpu_pll* h, size_t n, long* seg, long* warm);
@@ -357,7 +360,8 @@ int sdrgpu_biquad_process_dev(sdrgpu_biquad* h, const void* d_in, size_t ld_in, 
  * bit for bit against the true state and recomputed where they differ.  seg = warm = 0:
  * automatic (warm-up from the filter's slower pole, enough segments to fill the device, none
  * for Identity, an unstable design or a block that gives fewer than two); seg < 0: always
- * one serial pass.  Mirrors sdrgpu_pll_set_time_parallel. */
+ * one serial pass.  Mirrors sdrgpu_pll_set_time_parallel, in-place calls included (an output
+ * range overlapping the input runs one serial pass). */
 int sdrgpu_biquad_set_time_parallel(sdrgpu_biquad* h, long seg, long warm);
 /* the (segment, warm-up) a block of n samples per channel would use (segment 0: serial) */
 int sdrgpu_biquad_time_parallel_plan(const sdrgpu_biquad* h, size_t n, long* seg, long* warm);

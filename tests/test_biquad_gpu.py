@@ -171,3 +171,29 @@ def test_biquad_time_parallel_strided_device_rows(sdr, oracle):
         c = d.to_c()
         for ch in range(nch):
             np.testing.assert_array_equal(y[ch], oracle.biquad_run(c.kind, c.freq, c.q, RATE, x[ch]))
+
+
+def test_biquad_in_place_long_block(sdr, oracle):
+    """An in-place process_dev call (d_out == d_in) on a block long enough for the time-parallel
+    plan: the handle runs its serial pass (the segment kernels re-read inputs after outputs are
+    stored), so the result is still Biquad::apply's (biquad.rs:42-56), f32 and c64, state
+    carried into a second in-place block."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(78)
+    d = sdr.filter.BiquadD.LowPass(20000.0, 0.7)
+    for sk, dt in ((1, np.complex64), (0, np.float32)):
+        nch, n = 2, 400000
+        bq = d.design(RATE, sample_kind=sk, nch=nch)
+        assert bq.time_parallel_plan(n // 2)[0] > 0
+        x = _signal(rng, sk, nch, n)
+        halves = []
+        for h in range(2):
+            dx = DeviceBuffer.from_numpy(np.ascontiguousarray(x[:, h * (n // 2):(h + 1) * (n // 2)]))
+            bq.process_dev(dx.ptr, n // 2, n // 2, dx.ptr, n // 2)
+            bq.sync()
+            assert bq.last_time_parallel()[0] == 0  # serial pass
+            halves.append(dx.download(nch * (n // 2), dt).reshape(nch, n // 2))
+        y = np.concatenate(halves, axis=1)
+        c = d.to_c()
+        for ch in range(nch):
+            np.testing.assert_array_equal(y[ch], oracle.biquad_run(c.kind, c.freq, c.q, RATE, x[ch]))

@@ -187,22 +187,26 @@ def test_c4_matched_filter_into_pll_chain(sdr, oracle, nch, n, cut):
     assert lk.any() and out[lk.astype(bool)].std() > 0  # the chain locks and demodulates
 
 
-@pytest.mark.parametrize("K", [127, 255])
-def test_pll_beside_concurrent_mfma_bank(sdr, oracle, K):
+@pytest.mark.parametrize("K,n", [(127, 4096), (255, 4096), (127, 1 << 15), (255, 1 << 15)])
+def test_pll_beside_concurrent_mfma_bank(sdr, oracle, K, n):
     """The main.rs PLL (src/main.rs:41-46; src/filter/pll.rs:70-85) over 1024 channels while
     matched-filter bank launches (D = 1 MFMA kernel, src/filter/fir.rs:23-32 per channel) stream
-    over other buffers on another stream for the PLL's whole run.  K = 127 takes the bank
-    instantiation that leaves room for another wave on each of its SIMDs (176 VGPRs per wave).
-    Round 5 measured the PLL chain's packed-f32 mixer going wrong in lanes 48-63 when MFMA bank
-    waves shared its SIMD; the PLL kernels now claim their SIMD whole.  Outputs
-    and lock flags array_equal to the oracle PLL; the bank's last block within tolerance."""
+    over other buffers on another stream for the PLL's whole run.  n = 4096 runs the serial split
+    kernel; n = 2^15 is 8 segments of 4 Ki per channel, so the automatic plan runs the
+    time-parallel pll_seg / pll_refix / pll_fix kernels (configs[3]'s default) beside the bank.
+    Outputs and lock flags array_equal to the oracle PLL; the bank's last block within tolerance.
+    This is a concurrency smoke test, not the guard for the co-residency fault of DESIGN.md 3.6:
+    the shipped banks and PLL kernels cannot share a SIMD (both claim its register file), so it
+    cannot reproduce that fault; tests/test_kernel_resources_cpu.py checks the claims."""
     from sdrgpu.device import DeviceBuffer
     import scipy.signal as ss
     from test_pll_gpu import RATE, fm_channels, main_rs_design, oracle_params
-    rng = np.random.default_rng(500 + K)
-    nch, n = 1024, 4096
+    rng = np.random.default_rng(500 + K + n)
+    nch = 1024
     x = fm_channels(rng, nch, n)
     pll = main_rs_design(sdr).design(RATE, nch=nch)
+    tp = n >= 1 << 15
+    assert (pll.time_parallel_plan(n)[0] > 0) == tp
     dx = DeviceBuffer.from_numpy(x)
     do = DeviceBuffer.empty(nch * n, np.float32)
     dl = DeviceBuffer.empty(nch * n, np.uint8)
@@ -213,12 +217,14 @@ def test_pll_beside_concurrent_mfma_bank(sdr, oracle, K):
     dxb = DeviceBuffer.from_numpy(xb)
     dyb = DeviceBuffer.empty(nb_ch * nb, np.complex64)
     b.sync()
-    pll.process_dev(dx.ptr, n, n, do.ptr, dl.ptr, n)      # ~1.2 ms of PLL on its stream ...
+    pll.process_dev(dx.ptr, n, n, do.ptr, dl.ptr, n)      # the PLL on its stream ...
     reps = 24                                              # ... beside ~24 bank launches
     for _ in range(reps):
         assert b.process_dev(dxb.ptr, nb, nb, dyb.ptr, nb) == nb
     b.sync()
     pll.sync()
+    if tp:
+        assert pll.last_time_parallel()[0] == n // 4096  # segments per channel
     out = do.download(dtype=np.float32).reshape(nch, n)
     lk = dl.download(dtype=np.uint8).reshape(nch, n)
     ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)

@@ -1,10 +1,13 @@
-"""CPU check of the shipped code object (no GPU): the recurrence kernels that must own their
-SIMD do.  The PLL chain and the biquad bank claim the whole register file (512 VGPRs incl.
-AGPRs per wave, occupancy 1), so no wave of another kernel -- an MFMA FIR bank running on
-another stream -- can share their SIMD; round 5 measured wrong PLL results (lanes 48-63 of a
-packed-f32 mixer) when two MFMA bank waves shared the chain wave's SIMD (DESIGN.md 3.6,
-profiles/r05_chain_probe.txt).  Reads the amdhsa kernel metadata of libsdrgpu.so's gfx950 code
-objects with the ROCm LLVM tools."""
+"""CPU check of the shipped code object (no GPU): no wave of another kernel can share a SIMD with
+the MFMA FIR waves or with the recurrence kernels.  Round 5 measured wrong PLL results (lanes 48-63
+of a packed-f32 mixer) when two MFMA bank waves shared the chain wave's SIMD; round 6 traced the
+instruction pair (profiles/r06_hazard.txt).  Both sides claim the register file:
+  * the PLL and biquad kernels -- serial, split, and the time-parallel seg / refix / fix kernels
+    that configs[3] and main.rs run by default -- and the one-wave bf16x3 FIR (fir_mx_kernel)
+    allocate all 512 VGPRs (incl. AGPRs) of their SIMD;
+  * the two-waves-per-SIMD MFMA FIR kernels (fir_mxh_kernel, fir_mxi_kernel) allocate 256 VGPRs
+    and no AGPRs each, so the pair fills the SIMD.
+Reads the amdhsa kernel metadata of libsdrgpu.so's gfx950 code objects with the ROCm LLVM tools."""
 import os
 import re
 import struct
@@ -49,16 +52,35 @@ def kernel_registers(tmp_path):
     return regs
 
 
-@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")),
-                    reason="libsdrgpu.so not built or ROCm LLVM tools absent")
+NEEDS_LIB = pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")),
+                               reason="libsdrgpu.so not built or ROCm LLVM tools absent")
+RECURRENCE = re.compile(r"(pll_kernel|pll_split_kernel|pll_seg_kernel|pll_refix_kernel|pll_fix_kernel|"
+                        r"biquad_kernel|bq_seg_kernel|bq_refix_kernel|bq_fix_kernel)I")
+
+
+@NEEDS_LIB
 def test_recurrence_kernels_own_their_simd(tmp_path):
     regs = kernel_registers(tmp_path)
     assert len(regs) > 50, "kernel metadata not found"
-    own = {k: v for k, v in regs.items()
-           if re.search(r"pll_kernel|pll_split_kernel|biquad_kernel", k)}
-    assert len(own) >= 20, sorted(own)
-    small = {k: v for k, v in own.items() if max(v[0], v[0] + v[1] if v[0] <= 256 else 0) < 512}
-    assert not small, f"kernels that leave room on their SIMD: {small}"
-    # and the MFMA FIR kernels do not (two waves per SIMD by design)
-    fir = [v for k, v in regs.items() if "fir_mxh_kernel" in k]
-    assert fir and all(v[0] <= 256 for v in fir)
+    own = {k: v for k, v in regs.items() if RECURRENCE.search(k)}
+    # every family and instantiation: 8 PLL designs x (serial x2, split, seg x2, refix x2, fix x2)
+    # minus the split kernel's LDS-free variant axis, and 2 x 4 biquad kernels
+    for fam in ("pll_kernel", "pll_split_kernel", "pll_seg_kernel", "pll_refix_kernel",
+                "pll_fix_kernel", "biquad_kernel", "bq_seg_kernel", "bq_refix_kernel", "bq_fix_kernel"):
+        assert any(fam + "I" in k for k in own), f"{fam} not found in the code object"
+    assert len(own) >= 70, sorted(own)
+    small = {k: v for k, v in own.items() if v[0] < 512}
+    assert not small, f"recurrence kernels that leave room on their SIMD: {small}"
+
+
+@NEEDS_LIB
+def test_mfma_fir_kernels_fill_their_simd(tmp_path):
+    regs = kernel_registers(tmp_path)
+    pair = {k: v for k, v in regs.items() if re.search(r"(fir_mxh_kernel|fir_mxi_kernel)I", k)}
+    one = {k: v for k, v in regs.items() if "fir_mx_kernelI" in k}
+    assert len(pair) >= 14 and len(one) >= 6, (sorted(pair), sorted(one))
+    # two waves per SIMD (waves_per_eu(2, 2), 512-lane workgroups): 256 VGPRs and no AGPRs each
+    bad = {k: v for k, v in pair.items() if v != (256, 0)}
+    assert not bad, f"two-wave MFMA FIR kernels that leave room on their SIMD: {bad}"
+    bad = {k: v for k, v in one.items() if v[0] < 512}
+    assert not bad, f"one-wave MFMA FIR kernels that leave room on their SIMD: {bad}"

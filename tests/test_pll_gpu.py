@@ -399,3 +399,28 @@ def test_pll_time_parallel_auto_plan_configs3(sdr, oracle):
     ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), np.ascontiguousarray(x[chans]), nthreads=8)
     check(out[chans], lk[chans], ref_out, ref_lk, "configs[3] auto plan")
     assert np.array_equal(out[1], out[2]) and np.array_equal(out[1], out[1020])
+
+
+def test_pll_in_place_long_block(sdr, oracle):
+    """process_dev with the f32 outputs written over the c64 input rows (d_out = d_in,
+    ld_out = 2 ld_in: each output row inside its own input row) on a block the automatic plan
+    would cut into segments: the handle runs its serial pass (the segment kernels re-read inputs
+    after outputs are stored), so outputs and lock flags stay array_equal to the oracle
+    (src/filter/pll.rs:70-85), over two blocks with the state carried."""
+    from sdrgpu.device import DeviceBuffer
+    rng = np.random.default_rng(79)
+    nch, n = 64, 1 << 15
+    x = fm_channels(rng, nch, 2 * n)
+    pll = main_rs_design(sdr).design(RATE, nch=nch)
+    assert pll.time_parallel_plan(n)[0] > 0
+    outs, lks = [], []
+    for h in range(2):
+        dx = DeviceBuffer.from_numpy(np.ascontiguousarray(x[:, h * n:(h + 1) * n]))
+        dl = DeviceBuffer.empty(nch * n, np.uint8)
+        pll.process_dev(dx.ptr, n, n, dx.ptr, dl.ptr, 2 * n)
+        pll.sync()
+        assert pll.last_time_parallel()[0] == 0  # serial pass
+        outs.append(dx.download(nch * 2 * n, np.float32).reshape(nch, 2 * n)[:, :n])
+        lks.append(dl.download(dtype=np.uint8).reshape(nch, n))
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)
+    check(np.concatenate(outs, axis=1), np.concatenate(lks, axis=1), ref_out, ref_lk, "in place")

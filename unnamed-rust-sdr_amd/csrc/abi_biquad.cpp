@@ -68,9 +68,10 @@ struct sdrgpu_biquad {
         }
         if (n > sg) *seg = sg;
     }
-    int make_spec(long n, BqSpec* sp) {
+    int make_spec(long n, BqSpec* sp, bool serial = false) {
         plan(n, &sp->seg, &sp->warm);
         last_nseg = 0;
+        if (serial) sp->seg = 0;
         if (sp->seg <= 0) return SDRGPU_OK;
         sp->nseg = (n + sp->seg - 1) / sp->seg;
         long ck = sp->seg;  // checkpoints: at most 16 per segment, ck a multiple of 8 dividing seg
@@ -137,7 +138,9 @@ struct sdrgpu_biquad {
         if (n == 0) return SDRGPU_OK;
         if (!in || !out || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
         BqSpec sp;
-        int st = make_spec((long)n, &sp);
+        const size_t sb = sbytes();
+        const bool alias = bytes_overlap(in, rows_span(nch, ld_in, n, sb), out, rows_span(nch, ld_out, n, sb));
+        int st = make_spec((long)n, &sp, alias);
         if (st) return st;
         if (sp.seg > 0)
             return biquad_tp_launch(sk == SDRGPU_C64, (long)nch, c, in, (long)ld_in, (long)n, out,

@@ -142,5 +142,18 @@ int bq_design(const sdrgpu_biquad_design& d, float rate, float* c, int* ident);
 
 inline size_t kind_bytes(int kind) { return kind == SDRGPU_C64 ? 8 : (kind == SDRGPU_CU8 ? 2 : 4); }
 
+// Bytes spanned by rows rows of n elements (elem bytes each) with a leading dimension ld.
+inline size_t rows_span(size_t rows, size_t ld, size_t n, size_t elem) {
+    return rows ? ((rows - 1) * ld + n) * elem : 0;
+}
+// Whether the byte ranges [a, a + na) and [b, b + nb) overlap.  The time-parallel biquad and PLL
+// plans read input samples after outputs were stored (warm-ups reach into the previous segment;
+// the re-run and walk kernels re-read whole segments), so an in-place call takes the serial pass,
+// which reads every chunk before it stores it.
+inline bool bytes_overlap(const void* a, size_t na, const void* b, size_t nb) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+    return na && nb && x < y + nb && y < x + na;
+}
+
 }  // namespace detail
 }  // namespace sdrgpu

@@ -102,9 +102,10 @@ struct sdrgpu_pll {
         if (n > sg) *seg = sg;
     }
 
-    int make_spec(long n, PllSpec* sp) {
+    int make_spec(long n, PllSpec* sp, bool serial = false) {
         plan(n, &sp->seg, &sp->warm);
         last_nseg = 0;
+        if (serial) sp->seg = 0;
         if (sp->seg <= 0) return SDRGPU_OK;
         const long nseg = (n + sp->seg - 1) / sp->seg;
         // checkpoints every ck samples: at most 16 per segment, ck a multiple of 8 dividing seg
@@ -259,8 +260,12 @@ int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t
     if (!d_in || !d_out || !d_locked || ld_in < n || ld_out < n) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    // an output range overlapping the input takes the serial pass (bytes_overlap, abi_common.hpp)
+    const size_t nch = (size_t)h->dp.nch, in_bytes = rows_span(nch, ld_in, n, h->dp.in_u8 ? 2 : sizeof(float2));
+    const bool alias = bytes_overlap(d_in, in_bytes, d_out, rows_span(nch, ld_out, n, sizeof(float))) ||
+                       bytes_overlap(d_in, in_bytes, d_locked, rows_span(nch, ld_out, n, 1));
     PllSpec sp;
-    int st = h->make_spec((long)n, &sp);
+    int st = h->make_spec((long)n, &sp, alias);
     if (st) return st;
     return pll_launch(h->dp, d_in, (long)ld_in, (long)n, d_out, d_locked,
                       (long)ld_out, h->d_state, sp, h->stream.cur);

@@ -37,7 +37,7 @@ __device__ __forceinline__ float bq_step(const float* c, float x, float& x1, flo
 // SIMD (512 VGPRs claimed), so no MFMA wave of a concurrently running kernel can share it (the
 // measured hazard is described at pll.hip's own_simd).  One channel per lane, so this costs
 // nothing below 64 Ki channels.
-__device__ __forceinline__ void own_simd() { asm volatile("" ::: "v255", "a255"); }
+__device__ __forceinline__ void own_simd() { claim_simd_whole(); }
 
 template <bool CPLX>
 __global__ __launch_bounds__(kBqBlock) void biquad_kernel(long nch, float b0, float b1, float b2,

@@ -34,6 +34,17 @@ template <> __device__ __forceinline__ c64 zero_of<c64>() { return make_float2(0
 
 __host__ __device__ constexpr inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
+// -------- SIMD ownership --------
+// No wave of another kernel may share a SIMD with MFMA FIR waves: a packed-f32 VALU result was
+// read wrongly (lanes 48-63) by a PLL wave co-resident with MFMA bank waves.
+// A wave's register claim decides what else fits on its SIMD, so both sides claim the file:
+// the MFMA FIR kernels run two waves per SIMD and each names v255 (2 x 256 = 512 VGPRs, no
+// AGPRs), the one-wave-per-SIMD kernels (PLL, biquad, the bf16x3 FIR) name v255 and a255.
+// Only the kernel's VGPR count changes (the instruction stream is the same; checked by
+// tests/test_kernel_resources_cpu.py on the shipped code object).
+__device__ __forceinline__ void claim_simd_half() { asm volatile("" ::: "v255"); }
+__device__ __forceinline__ void claim_simd_whole() { asm volatile("" ::: "v255", "a255"); }
+
 }  // namespace sdrgpu
 
 // Host-side error plumbing shared by the ABI translation units.

@@ -94,6 +94,7 @@ void fir_mx_kernel(MxParams p) {
     constexpr int NP = 4 * NC;        // 16-byte pieces per lane per step
     static_assert(D % 2 == 0 && NCH % NC == 0, "geometry");
 
+    claim_simd_whole();  // one wave per SIMD, alone on it (common.hpp)
     const int lane = threadIdx.x & 63;
     const long wave = (long)blockIdx.x * (kMxBlock / 64) + (threadIdx.x >> 6);
     const int g = lane >> 4, v = lane & 15;

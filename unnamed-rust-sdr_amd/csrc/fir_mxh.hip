@@ -247,6 +247,7 @@ void fir_mxh_kernel(MxhParams p) {
     constexpr int TI = G::TI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
+    claim_simd_half();  // two waves fill the SIMD: nothing else shares it (common.hpp)
     const int lane = threadIdx.x & 63;
     // wave-uniform (readfirstlane), so the tile cursors and channel addressing stay scalar
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

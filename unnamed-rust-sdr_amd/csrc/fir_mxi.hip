@@ -156,6 +156,7 @@ void fir_mxi_kernel(MxiParams p) {
     constexpr int TI = G::TI, NG = G::NG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
+    claim_simd_half();  // two waves fill the SIMD: nothing else shares it (common.hpp)
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wv >= kWaves / 2) __builtin_amdgcn_s_setprio(1);

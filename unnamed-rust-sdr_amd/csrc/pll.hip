@@ -44,7 +44,7 @@ constexpr int kChunk = 8;       // samples per lane per pipeline stage
 // NCO value and the LDS hand-off were all right, and nothing in the ISA orders one wave's
 // VALU results against another wave's.  With the SIMD to itself the chain is bit-exact again,
 // at the same speed (a PLL wave alone on its SIMD is what it is sized for anyway).
-__device__ __forceinline__ void own_simd() { asm volatile("" ::: "v255", "a255"); }
+__device__ __forceinline__ void own_simd() { claim_simd_whole(); }
 
 struct Bq {
     float b0, b1, b2, na1, na2;
