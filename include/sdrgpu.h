@@ -297,7 +297,10 @@ int sdrgpu_pll_set_input_kind(sdrgpu_pll* h, int sample_kind);
  * true state exactly are re-run in parallel from their predecessor's end state and, where that
  * was not true either, recomputed from the true state.  seg = 0: automatic
  * (enough segments to give every SIMD one wave, none shorter than 4096 samples), seg < 0:
- * always one serial pass; warm = 0: 4096.  Lengths round up to multiples of 8.  A
+ * always one serial pass; warm = 0: 4096.  Lengths round up to multiples of 8.  The automatic
+ * plan adapts per handle: after a block in which more than half of the segments had to be
+ * recomputed (an unlocked loop, e.g. noise with no station), the next 8 blocks run one serial
+ * pass and the handle then tries segments again (reset starts over).  A
  * sdrgpu_pll_process_dev call whose output or lock range overlaps its input range (in place)
  * runs one serial pass whatever the plan (the segment kernels re-read inputs after outputs are
  * stored). */

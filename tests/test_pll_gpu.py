@@ -424,3 +424,31 @@ def test_pll_in_place_long_block(sdr, oracle):
         lks.append(dl.download(dtype=np.uint8).reshape(nch, n))
     ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)
     check(np.concatenate(outs, axis=1), np.concatenate(lks, axis=1), ref_out, ref_lk, "in place")
+
+
+def test_pll_time_parallel_adapts_to_noise(sdr, oracle):
+    """An unlocked loop (white noise, no carrier: src/filter/pll.rs:70-85 never converges bit for
+    bit from two starting states) under the automatic plan: the first block runs segments and
+    recomputes most of them, so the handle runs the next 8 blocks serially and then probes again
+    -- the plan sequence is (tp, 8 x serial, tp, ...) -- while every output stays array_equal to
+    the oracle; a locked FM block after reset() runs segments again."""
+    rng = np.random.default_rng(80)
+    nch, n, blocks = 64, 1 << 14, 10
+    pll = main_rs_design(sdr).design(RATE, nch=nch)
+    assert pll.time_parallel_plan(n)[0] > 0
+    x = ((rng.standard_normal((nch, n * blocks)) + 1j * rng.standard_normal((nch, n * blocks))) * 0.1).astype(np.complex64)
+    outs, lks, plan = [], [], []
+    for b in range(blocks):
+        o, lk = pll.process(x[:, b * n:(b + 1) * n])
+        segs, rec = pll.last_time_parallel()
+        plan.append((segs, rec))
+        outs.append(o)
+        lks.append(lk)
+    assert plan[0][0] > 0 and 2 * plan[0][1] > plan[0][0] * nch, plan[0]
+    assert all(p[0] == 0 for p in plan[1:9]), plan
+    assert plan[9][0] > 0, plan
+    ref_out, ref_lk = oracle.pll_batch(oracle_params(oracle), x, nthreads=16)
+    check(np.concatenate(outs, axis=1), np.concatenate(lks, axis=1), ref_out, ref_lk, "noise, adapted plan")
+    pll.reset()
+    pll.process(fm_channels(rng, nch, n))
+    assert pll.last_time_parallel()[0] > 0

@@ -76,6 +76,40 @@ struct sdrgpu_pll {
     DevBuf spec_buf;
     long last_nseg = 0;  // segments of the most recent time-parallel block (0: serial)
     long last_nck = 0;   // and the checkpoints per segment it kept
+    // Automatic plan, adapted per handle: when most segments of a time-parallel block had to be
+    // recomputed (an unlocked loop on noise: trajectories that never meet bit for bit), the next
+    // kSerialBlocks blocks run one serial pass and the handle then probes again.  The recompute
+    // count of each automatic time-parallel block is copied to pinned memory behind an event,
+    // and read by a later block's plan only once the event has completed (no stream sync).
+    static constexpr int kSerialBlocks = 8;
+    hipEvent_t probe_ev = nullptr;
+    unsigned long long* probe_host = nullptr;
+    bool probe_pending = false;
+    long probe_total = 0;
+    int serial_left = 0;
+
+    bool adapt_serial() {
+        if (tp_seg != 0) return false;
+        if (probe_pending && hipEventQuery(probe_ev) == hipSuccess) {
+            probe_pending = false;
+            if (2 * (long)*probe_host > probe_total) serial_left = kSerialBlocks;
+        }
+        if (serial_left > 0) {
+            --serial_left;
+            return true;
+        }
+        return false;
+    }
+    // after a launch: record this block's recompute count for the next plans
+    int probe(const PllSpec& sp) {
+        if (tp_seg != 0 || sp.seg <= 0 || probe_pending || !probe_ev) return SDRGPU_OK;
+        SDRGPU_HIP_TRY(hipMemcpyAsync(probe_host, sp.recomputed, sizeof(*probe_host), hipMemcpyDeviceToHost,
+                                      stream.cur));
+        SDRGPU_HIP_TRY(hipEventRecord(probe_ev, stream.cur));
+        probe_pending = true;
+        probe_total = last_nseg * dp.nch;
+        return SDRGPU_OK;
+    }
 
     // The plan for a block of n samples.  Auto: enough segments per channel to give every SIMD
     // one wave (64 channel-segments each), none shorter than 4 Ki samples, warm-up 4 Ki.  A
@@ -105,6 +139,7 @@ struct sdrgpu_pll {
     int make_spec(long n, PllSpec* sp, bool serial = false) {
         plan(n, &sp->seg, &sp->warm);
         last_nseg = 0;
+        if (sp->seg > 0 && adapt_serial()) serial = true;
         if (serial) sp->seg = 0;
         if (sp->seg <= 0) return SDRGPU_OK;
         const long nseg = (n + sp->seg - 1) / sp->seg;
@@ -138,6 +173,10 @@ struct sdrgpu_pll {
         DeviceGuard g(device);
         if (d_state) (void)hipFree(d_state);
         d_state = nullptr;
+        if (probe_ev) (void)hipEventDestroy(probe_ev);
+        probe_ev = nullptr;
+        if (probe_host) (void)hipHostFree(probe_host);
+        probe_host = nullptr;
         async.release();
         stage_in.release();
         stage_out.release();
@@ -155,6 +194,8 @@ int sdrgpu_pll_reset(sdrgpu_pll* h) {
     // PllDesign::design: nphase = 0, value = 0 + 0i, filter states zero (pll.rs:57-58)
     SDRGPU_HIP_TRY(hipMemsetAsync(h->d_state, 0, h->dp.nch * sizeof(PllChannelState), h->stream.cur));
     SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    h->probe_pending = false;  // the adapted plan starts over with the stream
+    h->serial_left = 0;
     return SDRGPU_OK;
 }
 
@@ -184,6 +225,9 @@ int sdrgpu_pll_create(int device, const sdrgpu_pll_params* p, size_t nch, sdrgpu
         if (!g.ok()) st = SDRGPU_ERR_DEVICE;
         if (!st) st = h->stream.create();
         if (!st && hipMalloc(&h->d_state, nch * sizeof(PllChannelState)) != hipSuccess) st = SDRGPU_ERR_NOMEM;
+        if (!st && (hipHostMalloc(reinterpret_cast<void**>(&h->probe_host), sizeof(*h->probe_host)) != hipSuccess ||
+                    hipEventCreateWithFlags(&h->probe_ev, hipEventDisableTiming) != hipSuccess))
+            st = SDRGPU_ERR_NOMEM;
         int cus = 0;
         if (!st && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
             cus > 0)
@@ -267,8 +311,10 @@ int sdrgpu_pll_process_dev(sdrgpu_pll* h, const void* d_in, size_t ld_in, size_t
     PllSpec sp;
     int st = h->make_spec((long)n, &sp, alias);
     if (st) return st;
-    return pll_launch(h->dp, d_in, (long)ld_in, (long)n, d_out, d_locked,
-                      (long)ld_out, h->d_state, sp, h->stream.cur);
+    if ((st = pll_launch(h->dp, d_in, (long)ld_in, (long)n, d_out, d_locked, (long)ld_out, h->d_state, sp,
+                         h->stream.cur)))
+        return st;
+    return h->probe(sp);
 }
 
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, float* out,
@@ -291,7 +337,7 @@ int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n, fl
                                     hipMemcpyHostToDevice, h->stream.cur));
     if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n,
                          static_cast<float*>(h->stage_out.ptr), static_cast<uint8_t*>(h->stage_lock.ptr),
-                         (long)n, h->d_state, sp, h->stream.cur)))
+                         (long)n, h->d_state, sp, h->stream.cur)) || (st = h->probe(sp)))
         return st;
     SDRGPU_HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(float), h->stage_out.ptr, n * sizeof(float),
                                     n * sizeof(float), nch, hipMemcpyDeviceToHost, h->stream.cur));
@@ -324,7 +370,7 @@ int sdrgpu_pll_process_async(sdrgpu_pll* h, const void* in, size_t n, float* out
     PllSpec sp;
     if ((st = h->make_spec((long)n, &sp))) return st;
     if ((st = pll_launch(h->dp, h->stage_in.ptr, (long)n, (long)n, d_out, d_lock, (long)n,
-                         h->d_state, sp, h->stream.cur)))
+                         h->d_state, sp, h->stream.cur)) || (st = h->probe(sp)))
         return st;
     if ((st = h->async.begin_download(h->stream.cur, slot))) return st;
     SDRGPU_HIP_TRY(hipMemcpyAsync(out, d_out, ob[0], hipMemcpyDeviceToHost, h->async.d2h));
