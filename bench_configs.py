@@ -385,10 +385,12 @@ def bench_c4(args):
     pll_v = f.PllDesign(0.0, 0.035, f.BiquadD.LowPass(80000.0, 0.7), f.Identity,
                         f.BiquadD.LowPass(20000.0, 0.7)).design(rate, nch=nch)
     pll_v.set_stream(bank.stream())
+    pll_v.set_phase_timing(True)
     plan = pll_v.time_parallel_plan(n)
     pll_v.process_dev(mf.ptr, n, n, out.ptr, lk.ptr, n)
     bank.sync()
     tp_segments, tp_recomputed = pll_v.last_time_parallel()
+    ph = pll_v.last_phase_ms()  # pass 1 / re-run pass / walk of that block (events on its stream)
     p = pyoracle.pll_params(0.0, 0.035, rate, (1, 80000.0, 0.7), (0, 0.0, 0.0), (1, 20000.0, 0.7))
     chans = sorted({0, nch // 3, nch // 2 + 1, nch - 1})
     mfs = np.stack([mf.download(n, offset_bytes=8 * c * n) for c in chans])
@@ -410,7 +412,8 @@ def bench_c4(args):
            "roofline": roof(12, units, ms), "fir_ms": round(ms_fir, 3), "pll_ms": round(ms - ms_fir, 3),
            "pll_ns_per_sample_chain": round((ms - ms_fir) * 1e6 / n, 2),
            "pll_plan": {"segment": plan[0], "warm": plan[1], "segments_per_channel": tp_segments,
-                        "segments_recomputed": tp_recomputed},
+                        "segments_recomputed": tp_recomputed,
+                        "phase_ms": {"pass1": round(ph[0], 3), "rerun": round(ph[1], 3), "walk": round(ph[2], 3)}},
            "pll_serial_ms": round(ms_serial, 3),
            "pll_serial_ns_per_sample_chain": round(ms_serial * 1e6 / n, 2),
            "note": "the PLL recurrence is serial per channel; time-parallel segments (speculative warm-up, exact verification, DESIGN.md 3.6) spread a channel over many SIMDs -- pll_ns_per_sample_chain is the wall time per sample of the whole batch",

@@ -310,6 +310,12 @@ int sdrgpu_pll_time_parallel_plan(const sdrgpu_pll* h, size_t n, long* seg, long
 /* The most recent block: its segment count (0 = serial) and how many segments had to be
  * recomputed from the true state (waits for the handle's stream). */
 int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recomputed);
+/* Measurement aid (no reference counterpart): with on != 0, time-parallel blocks record HIP
+ * events around their three kernels -- pass 1 (segments with warm-up), the parallel re-run pass
+ * and the per-channel walk -- and sdrgpu_pll_last_phase_ms returns the most recent block's
+ * three times in ms (all 0 for a serial block or with timing off; waits for the stream). */
+int sdrgpu_pll_set_phase_timing(sdrgpu_pll* h, int on);
+int sdrgpu_pll_last_phase_ms(sdrgpu_pll* h, float* pass1, float* rerun, float* walk);
 int sdrgpu_pll_set_stream(sdrgpu_pll* h, void* hip_stream);
 int sdrgpu_pll_get_stream(const sdrgpu_pll* h, void** hip_stream);
 int sdrgpu_pll_process(sdrgpu_pll* h, const void* in, size_t ld_in, size_t n,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a variant of libsdrgpu.so with extra compile flags on ONE source file:
 #   bash tools/diag/variant_build.sh NAME SOURCE.hip "FLAGS"  ->  tools/diag/probe_build/lib_NAME.so
-# (e.g. fir_mxh.hip "-DSDRGPU_MXR" for the role-split headline kernel).  The product library is
+# (e.g. fir_mxh.hip "-DSDRGPU_MXR=1" with tools/experiments/fir_mxh_rolesplit.patch applied).  The product library is
 # rebuilt first; the variant links every other product object unchanged.  Diagnostic only.
 set -e
 cd "$(dirname "$0")/../.."

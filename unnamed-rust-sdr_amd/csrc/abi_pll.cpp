@@ -87,6 +87,9 @@ struct sdrgpu_pll {
     bool probe_pending = false;
     long probe_total = 0;
     int serial_left = 0;
+    // sdrgpu_pll_set_phase_timing: events around the three kernels of a time-parallel block
+    hipEvent_t phase_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool phase_on = false;
 
     bool adapt_serial() {
         if (tp_seg != 0) return false;
@@ -164,6 +167,7 @@ struct sdrgpu_pll {
         sp->ckpt = nck ? sp->end2 + nstate : nullptr;
         sp->recomputed = reinterpret_cast<unsigned long long*>(sp->end2 + nstate + nck * nstate);
         sp->rstop = reinterpret_cast<int*>(sp->recomputed + 8);
+        sp->phase_ev = phase_on ? phase_ev : nullptr;
         last_nseg = nseg;
         last_nck = (long)nck;
         return SDRGPU_OK;
@@ -175,6 +179,10 @@ struct sdrgpu_pll {
         d_state = nullptr;
         if (probe_ev) (void)hipEventDestroy(probe_ev);
         probe_ev = nullptr;
+        for (auto& e : phase_ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         if (probe_host) (void)hipHostFree(probe_host);
         probe_host = nullptr;
         async.release();
@@ -282,6 +290,27 @@ int sdrgpu_pll_last_time_parallel(sdrgpu_pll* h, long* segments, long* recompute
                                  hipMemcpyDeviceToHost));
         *recomputed = (long)r;
     }
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_set_phase_timing(sdrgpu_pll* h, int on) {
+    if (!h) return SDRGPU_ERR_INVALID;
+    DeviceGuard g(h->device);
+    if (on && !h->phase_ev[0])
+        for (auto& e : h->phase_ev) SDRGPU_HIP_TRY(hipEventCreate(&e));
+    h->phase_on = on != 0;
+    return SDRGPU_OK;
+}
+
+int sdrgpu_pll_last_phase_ms(sdrgpu_pll* h, float* pass1, float* rerun, float* walk) {
+    if (!h || !pass1 || !rerun || !walk) return SDRGPU_ERR_INVALID;
+    *pass1 = *rerun = *walk = 0.f;
+    if (!h->phase_on || h->last_nseg <= 0) return SDRGPU_OK;
+    DeviceGuard g(h->device);
+    SDRGPU_HIP_TRY(hipStreamSynchronize(h->stream.cur));
+    SDRGPU_HIP_TRY(hipEventElapsedTime(pass1, h->phase_ev[0], h->phase_ev[1]));
+    SDRGPU_HIP_TRY(hipEventElapsedTime(rerun, h->phase_ev[1], h->phase_ev[2]));
+    SDRGPU_HIP_TRY(hipEventElapsedTime(walk, h->phase_ev[2], h->phase_ev[3]));
     return SDRGPU_OK;
 }
 

@@ -64,9 +64,6 @@ constexpr int kCs2 = 2;
 // within noise there).
 constexpr int kRunTiles = 2;
 constexpr int kRunTilesU8 = 8;
-#ifndef RS_PRIO
-#define RS_PRIO 1
-#endif
 
 // CS: 256-output MFMA column sets per tile.  D = 1 stages the window's history once for CS
 // column sets (the history is 1.5x a 256-sample set, so re-staging it per set dominated)
@@ -636,300 +633,6 @@ void fir_mxh_kernel(MxhParams p) {
     }
 }
 
-// ---- Role split (round 6): staging waves and one MFMA wave per SIMD ----
-// The c64 D = 4 tiles of fir_mxh_kernel, with the waves of each SIMD given one job each instead
-// of every wave doing everything: NS *stagers* per SIMD load raw tiles (two in flight each), take
-// the window max, split and write windows into a ring of kRsSlots windows in LDS (stager s of a
-// SIMD stages tiles s, s + NS, ... of the SIMD's stream); the SIMD's *MFMA wave* reads the B
-// fragments, runs the 60 MFMAs of each tile, rescales and stores.  Windows are handed over
-// through LDS words (release store / acquire load, workgroup scope, no barriers): per slot the
-// index + 1 of the tile staged into it, and `done` = tiles whose fragment reads are complete.
-// Every window stages its own history (no sticky scale).  Same arithmetic as fir_mxh_kernel.
-constexpr int kRsSlots = 3;
-// bound on a hand-over wait (s_sleep 1 each, ~0.1 s in all): every wait is met within a tile's
-// time by construction; the bound only guarantees that the grid drains if that were broken
-constexpr int kRsSpin = 1 << 21;
-
-template <int NCH>
-struct GeoR {
-    using G = GeoH<NCH, 4, 1>;
-    static constexpr int WS = G::H + G::TI;     // window samples (history + new)
-    static constexpr int PLB = 2 * WS;          // bytes per fp16 plane
-    static constexpr int SLOT = 4 * PLB;        // bytes per window
-    static constexpr int PAIR = kRsSlots * SLOT;
-    static constexpr int FLAGS = 4 * PAIR;      // then 64 B per SIMD: ready[slots], done, scale[slots]
-    static constexpr int LDS = FLAGS + 4 * 64;
-    static_assert(LDS <= 160 * 1024 && SLOT % 128 == 0 && 1 + 2 * kRsSlots <= 16, "LDS");
-};
-
-__device__ __forceinline__ int lds_acquire(const int* a) {
-    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_release(int* a, int v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int NCH, int NS>
-__global__ __launch_bounds__(256 * (1 + NS)) __attribute__((amdgpu_waves_per_eu(1 + NS, 1 + NS)))
-void fir_mxr_kernel(MxhParams p) {
-    using G = GeoH<NCH, 4, 1>;
-    using R = GeoR<NCH>;
-    constexpr int H = G::H, HR = G::HR, NH = G::NH, NG = G::NG, TI = G::TI, PLB = R::PLB;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if constexpr (NS == 1) claim_simd_half();
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pr = wv & 3;               // the SIMD (waves are dealt to SIMDs round robin)
-    const bool mfma_wave = wv < 4;
-    int* fl = reinterpret_cast<int*>(smem + R::FLAGS + 64 * pr);
-    int* const ready = fl;               // [kRsSlots]
-    int* const done = fl + kRsSlots;
-    int* const scale = fl + kRsSlots + 1;  // [kRsSlots]
-    if (threadIdx.x < 64) reinterpret_cast<int*>(smem + R::FLAGS)[threadIdx.x] = 0;
-    __syncthreads();
-    const int K = p.K;
-    const long n_in = p.n_in;
-
-    // the SIMD's tile stream: units of seg_tiles tiles dealt grid-strided over the SIMDs
-    struct Cur {
-        int u, t, ch, tu, nt;
-        bool ok;
-    };
-    const int units = (int)p.units, spc = (int)p.spc, segt = (int)p.seg_tiles, tpc = (int)p.tpc;
-    const int nq = (int)gridDim.x * 4;
-    auto seek = [&](Cur& c, int u) __attribute__((always_inline)) {
-        c.u = u;
-        c.t = 0;
-        c.ok = u < units;
-        c.ch = c.ok && spc < units ? u / spc : 0;
-        c.tu = (u - c.ch * spc) * segt;
-        c.nt = c.ok ? std::min(segt, tpc - c.tu) : 0;
-        if (c.ok && c.nt <= 0) c.ok = false;
-    };
-    auto adv = [&](Cur& c) __attribute__((always_inline)) {
-        if (!c.ok) return;
-        if (++c.t >= c.nt) seek(c, c.u + nq);
-    };
-    auto tile_j0 = [&](const Cur& c) __attribute__((always_inline)) { return (long)TI * (c.tu + c.t); };
-    const int q0 = (int)blockIdx.x * 4 + pr;
-
-    if (!mfma_wave) {
-        // ---------------- stager s of SIMD pr: tiles s, s + NS, ... ----------------
-        const int sid = NS == 1 ? 0 : (wv >> 2) - 1;
-        auto fetch = [&](const Cur& c, long j) __attribute__((always_inline)) {
-            return fetch_pair(p.in + c.ch * p.ld_in, p.hist + c.ch * (long)(K - 1), j, n_in, K);
-        };
-        // stream start / end only (guarded, synchronous): kept out of the prefetch so every
-        // issue() below is the same NH + NG loads and the waits stay counted (vmcnt(NH + NG))
-        auto load_tile_slow = [&](float4 (&dst)[NG], const Cur& c) __attribute__((always_inline)) {
-            asm volatile("" ::: "memory");
-            const long j0 = tile_j0(c);
-#pragma unroll
-            for (int k = 0; k < NG; ++k) dst[k] = fetch(c, j0 + 128 * k + 2 * lane);
-        };
-        auto load_hist_slow = [&](float4 (&dst)[NH], const Cur& c) __attribute__((always_inline)) {
-            asm volatile("" ::: "memory");
-            const long j = tile_j0(c) - H;
-#pragma unroll
-            for (int k = 0; k < NH; ++k) dst[k] = fetch(c, j + 128 * k + 2 * lane);
-        };
-        auto hist_fast = [&](const Cur& c) __attribute__((always_inline)) {
-            const int tile = c.tu + c.t;  // j >= 0 and j + H <= n_in (H <= TI)
-            return tile >= 1 && tile <= p.ftiles;
-        };
-        // with one stager a continuing tile's history is the previous tile's tail (registers);
-        // with several, every tile loads its history (the other stager streamed it: L2)
-        auto hist_loaded = [&](const Cur& c) __attribute__((always_inline)) { return NS > 1 || c.t == 0; };
-        // the prefetch of tile c: NH history groups and NG groups, from the zeroed dummy tile
-        // where the real ones are not wholly inside the input (or not needed)
-        auto issue = [&](float4 (&nx)[NG], float4 (&hh)[NH], const Cur& c) __attribute__((always_inline)) {
-            const long j0 = tile_j0(c);
-            const float2* base = p.in + c.ch * p.ld_in;
-            const float2* src = c.ok && c.tu + c.t < p.ftiles ? base + j0 : p.dummy;
-            const float2* hsrc = c.ok && hist_loaded(c) && hist_fast(c) ? base + j0 - H : p.dummy;
-#pragma unroll
-            for (int k = 0; k < NH; ++k) {
-                const f32x4 r = *reinterpret_cast<const f32x4*>(hsrc + 128 * k + 2 * lane);
-                hh[k] = make_float4(r[0], r[1], r[2], r[3]);
-            }
-#pragma unroll
-            for (int k = 0; k < NG; ++k) {
-                const f32x4 r = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 128 * k + 2 * lane));
-                nx[k] = make_float4(r[0], r[1], r[2], r[3]);
-            }
-        };
-        auto step = [&](Cur& c) __attribute__((always_inline)) {
-#pragma unroll
-            for (int i = 0; i < NS; ++i) adv(c);
-        };
-        const int wb0 = 128 * (lane >> 5) + 4 * (lane & 3) + 16 * ((lane >> 2) & 7);
-        Cur ld, st;
-        seek(ld, q0);
-#pragma unroll
-        for (int i = 0; i < NS - 1; ++i)
-            if (i < sid) adv(ld);
-        st = ld;
-        float4 raw[2][NG], hist[2][NH], tail[NH];
-        issue(raw[0], hist[0], ld);
-        step(ld);
-        __builtin_amdgcn_sched_barrier(0);  // raw[0]'s loads stay the older ones (counted waits)
-        issue(raw[1], hist[1], ld);
-        step(ld);
-        int it = sid;
-        auto body = [&](auto par_c) __attribute__((always_inline)) {
-            constexpr int PAR = decltype(par_c)::value;
-            float4(&nx)[NG] = raw[PAR];
-            float4(&hh)[NH] = hist[PAR];
-            if (st.tu + st.t >= p.ftiles) load_tile_slow(nx, st);
-            // the window's history: loaded with the tile, or the staged tile's tail (a uniform
-            // branch of whole copies: a select of two arrays would take their addresses and keep
-            // them out of registers)
-            if (hist_loaded(st)) {
-                if (!hist_fast(st)) load_hist_slow(hh, st);
-#pragma unroll
-                for (int k = 0; k < NH; ++k) tail[k] = hh[k];
-            }
-            float m = 0.f;
-#pragma unroll
-            for (int k = 0; k < NG; ++k) m = absmax4(m, nx[k]);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) m = absmax4(m, tail[k]);
-            const int s = wave_scale(m);
-            const float sc = exp2i(s);
-            const int slot = it % kRsSlots;
-            const int sb = pr * R::PAIR + slot * R::SLOT;
-            for (int spin = 0; lds_acquire(done) < it - kRsSlots + 1 && spin < kRsSpin; ++spin)
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) put_pair<PLB>(smem, sb + (wb0 ^ (16 * (k & 7))) + 256 * k, tail[k], sc);
-#pragma unroll
-            for (int k = NH; k < NH + NG; ++k)
-                put_pair<PLB>(smem, sb + (wb0 ^ (16 * (k & 7))) + 256 * k, nx[k - NH], sc);
-            scale[slot] = s;
-            lds_release(ready + slot, it + 1);
-#pragma unroll
-            for (int k = 0; k < NH; ++k) tail[k] = nx[NG - NH + k];
-            it += NS;
-            step(st);
-            issue(nx, hh, ld);
-            step(ld);
-        };
-        while (st.ok) {
-            body(std::integral_constant<int, 0>());
-            if (!st.ok) break;
-            body(std::integral_constant<int, 1>());
-        }
-    } else {
-        // ---------------- MFMA wave ----------------
-        const int g = lane >> 4, v = lane & 15;
-        u32x4 ah[NCH], al[NCH];
-        {
-            const float tsc = exp2i(p.sh);
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    unsigned hw = 0, lw = 0;
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const int pidx = 32 * c + 8 * g + 2 * jj + e;
-                        const int k = 4 * v + 3 - p.delta + HR - pidx;
-                        const bool ok = (k >= 0) & (k < K);
-                        const float hk = p.taps[ok ? k : 0];
-                        const float hs = ok ? hk * tsc : 0.f;
-                        const _Float16 h16 = (_Float16)hs;
-                        const _Float16 l16 = (_Float16)(hs - (float)h16);
-                        hw |= (unsigned)__builtin_bit_cast(unsigned short, h16) << (16 * e);
-                        lw |= (unsigned)__builtin_bit_cast(unsigned short, l16) << (16 * e);
-                    }
-                    ah[c][jj] = hw;
-                    al[c][jj] = lw;
-                }
-            }
-        }
-        const int sv = sigma(v);
-        int rb[NCH];
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int r = sv + (c >> 1);
-            rb[c] = pr * R::PAIR + 128 * r + 16 * ((4 * (c & 1) + g) ^ ((r >> 1) & 7));
-        }
-        const bool ev = (v & 1) == 0;
-        const unsigned om = 8u * (16 * sv + 4 * g), omp = 8u * (16 * sigma(v ^ 1) + 4 * g);
-        const unsigned ob1 = ev ? om : omp + 16, ob2 = ev ? omp : om + 16;
-        if (RS_PRIO) __builtin_amdgcn_s_setprio(1);
-        Cur cm;
-        seek(cm, q0);
-        int it = 0;
-        while (cm.ok) {
-            const int slot = it % kRsSlots;
-            for (int spin = 0; lds_acquire(ready + slot) <= it && spin < kRsSpin; ++spin)
-                __builtin_amdgcn_s_sleep(1);
-            const int s_cur = __builtin_amdgcn_readfirstlane(scale[slot]);
-            const int so = slot * R::SLOT;
-            f32x4 cr = {0.f, 0.f, 0.f, 0.f}, ci = {0.f, 0.f, 0.f, 0.f};
-            u32x4 fb[2][4];
-            auto read_frags = [&](u32x4 (&f)[4], int c) __attribute__((always_inline)) {
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd)
-                    f[qd] = *reinterpret_cast<const u32x4*>(smem + rb[c] + so + qd * PLB);
-            };
-            read_frags(fb[0], 0);
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                if (c + 1 < NCH) read_frags(fb[(c + 1) & 1], c + 1);
-                __builtin_amdgcn_sched_barrier(0);
-                const u32x4(&f)[4] = fb[c & 1];
-                cr = mfma(al[c], f[0], cr);
-                ci = mfma(al[c], f[2], ci);
-                cr = mfma(ah[c], f[1], cr);
-                ci = mfma(ah[c], f[3], ci);
-                cr = mfma(ah[c], f[0], cr);
-                ci = mfma(ah[c], f[2], ci);
-            }
-            lds_release(done, it + 1);
-            const int sh_out = -(s_cur + p.sh);
-            const int tile = cm.tu + cm.t;
-            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            char* __restrict__ outt = reinterpret_cast<char*>(out + (long)tile * G::TO);
-            float yr[4], yi[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                yr[i] = __builtin_amdgcn_ldexpf(cr[i], sh_out);
-                yi[i] = __builtin_amdgcn_ldexpf(ci[i], sh_out);
-            }
-            if (p.vec_out && tile < p.oblk) {
-                const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                f32x4 rx;
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd)
-                    rx[qd] = __int_as_float(__builtin_amdgcn_mov_dpp(
-                        __float_as_int(ev ? y1[qd] : y0[qd]), 0xB1, 0xf, 0xf, false));
-                __builtin_nontemporal_store(ev ? y0 : rx, reinterpret_cast<f32x4*>(outt + ob1));
-                __builtin_nontemporal_store(ev ? rx : y1, reinterpret_cast<f32x4*>(outt + ob2));
-            } else {
-                const long mo = (long)tile * G::TO + 16 * sv + 4 * g;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (mo + i < p.n_out) out[mo + i] = make_float2(yr[i], yi[i]);
-            }
-            ++it;
-            adv(cm);
-        }
-    }
-
-    if (p.hist_next) {  // stream history carry, spread over the whole grid
-        const long nch = p.units / p.spc;
-        const int nthr = 256 * (1 + NS);
-        for (long j = (long)blockIdx.x * nthr + threadIdx.x; j < nch * (K - 1); j += (long)gridDim.x * nthr) {
-            const long ch = j / (K - 1), jj = j - ch * (K - 1);
-            const long gidx = p.n_in - (long)(K - 1) + jj;
-            p.hist_next[j] = gidx >= 0 ? p.in[ch * p.ld_in + gidx] : p.hist[ch * (long)(K - 1) + gidx + (K - 1)];
-        }
-    }
-}
-
 int mxh_nch(int K, int D) {
     if (D == 4) {
         const int need = (K + 63 + 31) / 32;  // 32 NCH >= K + 15*4 + 3
@@ -1015,18 +718,6 @@ int fir_mxh_launch(const FirParams& fp, const float* d_taps, int tap_scale_exp,
     // 32-bit tile cursors (units, tiles per channel, unit / tile indices)
     if (p.units >= INT_MAX - 8L * cus || p.tpc >= INT_MAX) return SDRGPU_ERR_UNSUPPORTED;
     const long blocks = std::max(1L, std::min((long)cus, ceil_div(p.units, kWaves)));
-#ifdef SDRGPU_MXR
-    if (D == 4 && !u8) {  // role split: per SIMD one MFMA wave and SDRGPU_MXR stagers
-        constexpr int NS = SDRGPU_MXR;
-        const long rblocks = std::max(1L, std::min((long)cus, ceil_div(p.units, 4L)));
-        if (NCH == 10)
-            hipLaunchKernelGGL((fir_mxr_kernel<10, NS>), dim3(rblocks), dim3(256 * (1 + NS)), (size_t)GeoR<10>::LDS, s, p);
-        else
-            hipLaunchKernelGGL((fir_mxr_kernel<6, NS>), dim3(rblocks), dim3(256 * (1 + NS)), (size_t)GeoR<6>::LDS, s, p);
-        SDRGPU_LAUNCH_CHECK();
-        return SDRGPU_OK;
-    }
-#endif
 #define SDRGPU_MXH_GO(CC, U, DD, CS)                                                           \
     hipLaunchKernelGGL((fir_mxh_kernel<CC, U, DD, CS>), dim3(blocks), dim3(kBlock),            \
                        (size_t)kWaves * (GeoH<CC, DD, CS>::WAVE), s, p)

@@ -573,17 +573,21 @@ void launch_cfg(const PllDevParams& p, const void* in, long ld_in, long n, float
         const long nseg = (n + spec.seg - 1) / spec.seg;
         const long sblk = (p.nch * nseg + kPllBlock - 1) / kPllBlock;
 #define SDRGPU_PLL_SEG(V)                                                                          \
+        if (spec.phase_ev) (void)hipEventRecord(spec.phase_ev[0], s);                              \
         hipLaunchKernelGGL((pll_seg_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
                            spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.ck, spec.ckpt);    \
+        if (spec.phase_ev) (void)hipEventRecord(spec.phase_ev[1], s);                              \
         hipLaunchKernelGGL((pll_refix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)sblk),    \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, spec.seg,   \
                            spec.warm, nseg, spec.guess, spec.end, spec.ck, spec.ckpt, spec.rstop,   \
                            spec.end2);                                                              \
+        if (spec.phase_ev) (void)hipEventRecord(spec.phase_ev[2], s);                              \
         hipLaunchKernelGGL((pll_fix_kernel<U8, LID, OID, KID, MODE, V>), dim3((unsigned)nblk),      \
                            dim3(kPllBlock), 0, s, p, in, ld_in, n, out, locked, ld_out, state,       \
                            spec.seg, spec.warm, nseg, spec.guess, spec.end, spec.recomputed,        \
-                           spec.ck, spec.ckpt, spec.rstop, spec.end2)
+                           spec.ck, spec.ckpt, spec.rstop, spec.end2);                              \
+        if (spec.phase_ev) (void)hipEventRecord(spec.phase_ev[3], s)
         if (vec) { SDRGPU_PLL_SEG(true); } else { SDRGPU_PLL_SEG(false); }
 #undef SDRGPU_PLL_SEG
         return;

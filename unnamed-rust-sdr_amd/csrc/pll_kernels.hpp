@@ -41,6 +41,8 @@ struct PllSpec {
     // state in end2), 0 = not re-run
     int* rstop = nullptr;
     PllChannelState* end2 = nullptr;
+    // optional: four events recorded around pass 1, the re-run pass and the walk
+    hipEvent_t* phase_ev = nullptr;
 };
 
 int pll_launch(const PllDevParams& p, const void* in, long ld_in, long n, float* out,

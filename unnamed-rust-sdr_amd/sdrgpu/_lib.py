@@ -166,6 +166,8 @@ SIGNATURES = [
     ("sdrgpu_pll_set_time_parallel", c_int, [_H, c_long, c_long]),
     ("sdrgpu_pll_time_parallel_plan", c_int, [_H, c_size_t, POINTER(c_long), POINTER(c_long)]),
     ("sdrgpu_pll_last_time_parallel", c_int, [_H, POINTER(c_long), POINTER(c_long)]),
+    ("sdrgpu_pll_set_phase_timing", c_int, [_H, c_int]),
+    ("sdrgpu_pll_last_phase_ms", c_int, [_H, POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
     ("sdrgpu_pll_set_stream", c_int, [_H, c_void_p]),
     ("sdrgpu_pll_get_stream", c_int, [_H, _PH]),
     ("sdrgpu_pll_process", c_int,

@@ -525,6 +525,17 @@ class Pll:
               "sdrgpu_pll_last_time_parallel")
         return a.value, b.value
 
+    def set_phase_timing(self, on: bool = True):
+        """Record events around the three kernels of time-parallel blocks (measurement aid)."""
+        check(lib().sdrgpu_pll_set_phase_timing(self._h, 1 if on else 0), "sdrgpu_pll_set_phase_timing")
+
+    def last_phase_ms(self):
+        """(pass 1, re-run pass, walk) ms of the most recent block (zeros when serial)."""
+        a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        check(lib().sdrgpu_pll_last_phase_ms(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+              "sdrgpu_pll_last_phase_ms")
+        return a.value, b.value, c.value
+
     def time_parallel_plan(self, n: int):
         """(segment length or 0 for one serial pass, warm-up) for a block of n samples."""
         seg, warm = ctypes.c_long(), ctypes.c_long()
