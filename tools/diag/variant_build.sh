@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build a variant of libsdrgpu.so with extra compile flags on ONE source file:
-#   bash tools/diag/variant_build.sh NAME SOURCE.hip "FLAGS"  ->  tools/diag/probe_build/lib_NAME.so
+#   bash tools/diag/variant_build.sh NAME SOURCE.hip "FLAGS"  ->  tools/diag/var_build/lib_NAME.so (git-ignored; travels with the snapshot)
 # (e.g. fir_mxh.hip "-DSDRGPU_MXR=1" with tools/experiments/fir_mxh_rolesplit.patch applied).  The product library is
 # rebuilt first; the variant links every other product object unchanged.  Diagnostic only.
 set -e
 cd "$(dirname "$0")/../.."
 make -C unnamed-rust-sdr_amd -s
-O=tools/diag/probe_build
+O=tools/diag/var_build
 mkdir -p $O
 src=$2
 obj=$(basename ${src%.hip}).o

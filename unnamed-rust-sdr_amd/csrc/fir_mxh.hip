@@ -223,8 +223,11 @@ __device__ __forceinline__ int wave_scale(float m) {
     const unsigned a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
     const unsigned c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
     const unsigned ab = a > b ? a : b, cd = c > d ? c : d;
-    // 15 - frexp exponent = 141 - biased exponent for a normal max; a zero / subnormal max
-    // clamps to 126 as frexp's exponent would; inf / NaN (biased 255) keep frexp's 0 -> 15
+    // 15 - frexp exponent = 141 - biased exponent for a normal max; a zero or subnormal max
+    // (biased 0) gives 141, clamped to 126 (round 4's v_frexp_exp form gave 15 for an exact zero:
+    // an all-zero window's outputs are zero either way, but the sticky-scale keep / restage
+    // choice of the odd tile after it can differ, so its low bits are not round 4's); inf / NaN
+    // (biased 255) keep frexp's 0 -> 15
     const int e = (int)((ab > cd ? ab : cd) >> 23);
     const int s = e == 255 ? 15 : 141 - e;
     return s < -126 ? -126 : (s > 126 ? 126 : s);
