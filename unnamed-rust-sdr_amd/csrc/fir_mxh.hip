@@ -64,6 +64,13 @@ constexpr int kCs2 = 2;
 // within noise there).
 constexpr int kRunTiles = 2;
 constexpr int kRunTilesU8 = 8;
+// Staging schedule: the next window's groups are split and written kStagePerChunk per MFMA chunk
+// (groups 0-3 after chunk 0, 4-7 after chunk 1), so the raw-tile loads that reuse their
+// registers are issued early in the body and have most of it to land.  Round 6, alternating
+// same-box A/Bs (profiles/r06_stage_burst_ab.txt), outputs bit-identical to one group per chunk:
+// configs[1] steady state 0.4400 -> 0.4289 ms (2 per chunk 0.4323, 8 0.4346), driver window
+// 0.501 -> 0.504 ms (noise); configs[4] bank 1.967 -> 1.954 ms in the window.
+constexpr int kStagePerChunk = 4;
 
 // CS: 256-output MFMA column sets per tile.  D = 1 stages the window's history once for CS
 // column sets (the history is 1.5x a 256-sample set, so re-staging it per set dominated)
@@ -539,7 +546,7 @@ void fir_mxh_kernel(MxhParams p) {
                 }
 #pragma unroll
                 for (int k = 0; k < NG; ++k) {
-                    if ((k < CS * NCH - 1 ? k : CS * NCH - 1) != i) continue;
+                    if ((k / kStagePerChunk < CS * NCH - 1 ? k / kStagePerChunk : CS * NCH - 1) != i) continue;
                     // an even window's last NH groups overlap the odd window being read: later
                     if (P == 1 || k < NG - NH) put(WN + new_addr(k), nx[k], scn);
                     if (k >= NG - NH) keep[k - (NG > NH ? NG - NH : 0)] = nx[k];
