@@ -141,6 +141,11 @@ int sdrgpu_fir_get_stream(const sdrgpu_fir* h, void** hip_stream);
 int sdrgpu_fir_output_len(const sdrgpu_fir* h, size_t n_in, size_t* n_out);
 int sdrgpu_fir_process(sdrgpu_fir* h, const void* in, size_t n_in, void* out,
                        size_t out_cap, size_t* n_out);
+/* DEVICE pointers, enqueued on the handle's stream.  d_out may overlap d_in (in place, or
+ * shifted): the handle then filters a device copy of the input, so the results are those of an
+ * out-of-place call (the kernels store output tiles while other workgroups still read the
+ * input under them).  The same holds for sdrgpu_firbank_process_dev, sdrgpu_fft_exec_dev,
+ * sdrgpu_rfft_exec_dev and sdrgpu_stft_process_dev. */
 int sdrgpu_fir_process_dev(sdrgpu_fir* h, const void* d_in, size_t n_in, void* d_out,
                            size_t out_cap, size_t* n_out);
 /* HOST pointers, asynchronous (the Block adapter's producer/consumer split,

@@ -154,6 +154,20 @@ inline bool bytes_overlap(const void* a, size_t na, const void* b, size_t nb) {
     const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
     return na && nb && x < y + nb && y < x + na;
 }
+// The FIR, FFT and STFT kernels store output tiles while other workgroups still read the input
+// under them, so a device input range that overlaps the call's output range is copied to `stage`
+// (on the call's stream, ahead of the kernels) and the copy is read instead: in-place calls give
+// the results of out-of-place ones, at the cost of one device copy of the input.
+inline int unalias_input(DevBuf& stage, const void*& in, size_t in_bytes, const void* out,
+                         size_t out_bytes, hipStream_t s) {
+    if (!bytes_overlap(in, in_bytes, out, out_bytes)) return SDRGPU_OK;
+    const int st = stage.ensure(in_bytes);
+    if (st) return st;
+    if (hipMemcpyAsync(stage.ptr, in, in_bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return SDRGPU_ERR_DEVICE;
+    in = stage.ptr;
+    return SDRGPU_OK;
+}
 
 }  // namespace detail
 }  // namespace sdrgpu

@@ -15,7 +15,7 @@ struct sdrgpu_fft {
     int out_db = 0;  // SDRGPU_FFT_OUT_DB: f32 dB magnitudes instead of C64 values
     void* plan = nullptr;
     StreamSlot stream;
-    DevBuf stage_in, stage_out, scratch;
+    DevBuf stage_in, stage_out, scratch, alias;  // alias: copy of an input the output overlaps
     AsyncD2H async;
     size_t out_elem() const { return out_db ? sizeof(float) : sizeof(float2); }
 
@@ -29,6 +29,7 @@ struct sdrgpu_fft {
         stage_in.release();
         stage_out.release();
         scratch.release();
+        alias.release();
         async.release();
         if (plan) fft_plan_destroy(plan);
         plan = nullptr;
@@ -108,6 +109,9 @@ int sdrgpu_fft_exec_dev(sdrgpu_fft* h, const void* d_in, void* d_out, size_t cou
     if (!d_in || !d_out) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    int st = unalias_input(h->alias, d_in, count * (size_t)h->n * sizeof(float2), d_out,
+                           count * (size_t)h->n * h->out_elem(), h->stream.cur);
+    if (st) return st;
     FftFrames fr{};
     fr.mode = 0;
     fr.in = static_cast<const float2*>(d_in);
@@ -138,9 +142,13 @@ int sdrgpu_rfft_exec_dev(sdrgpu_fft* h, const float* d_in, void* d_out, size_t c
     if (!d_in || !d_out) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    const void* in = d_in;
+    int st = unalias_input(h->alias, in, count * (size_t)h->n * sizeof(float), d_out,
+                           count * (size_t)(h->n - h->n / 2) * h->out_elem(), h->stream.cur);
+    if (st) return st;
     FftFrames fr{};
     fr.mode = 2;
-    fr.in_real = d_in;
+    fr.in_real = static_cast<const float*>(in);
     fr.nframes = (long)count;
     return h->run(fr, static_cast<float2*>(d_out), 1);
 }
@@ -246,6 +254,10 @@ int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void*
     if (!d_in || (nf && !d_out)) return SDRGPU_ERR_INVALID;
     DeviceGuard g(h->fft.device);
     if (!g.ok()) return SDRGPU_ERR_DEVICE;
+    // the frames are stored before the carry kernel re-reads the input's tail
+    int st = unalias_input(h->fft.alias, d_in, n_in * kind_bytes(h->in_kind), d_out,
+                           nf * (size_t)h->fft.n * h->fft.out_elem(), h->fft.stream.cur);
+    if (st) return st;
     FftFrames fr{};
     const bool u8 = h->in_kind == SDRGPU_CU8;
     fr.mode = u8 ? 3 : 1;
@@ -257,7 +269,7 @@ int sdrgpu_stft_process_dev(sdrgpu_stft* h, const void* d_in, size_t n_in, void*
     fr.first_end = h->first_end();
     fr.hop = h->hop;
     fr.nframes = (long)nf;
-    int st = h->fft.run(fr, static_cast<float2*>(d_out), 0);
+    st = h->fft.run(fr, static_cast<float2*>(d_out), 0);
     if (st) return st;
     st = u8 ? stft_carry_u8_launch(fr.in_u8, fr.n_in, h->d_hist[h->cur], h->d_hist[h->cur ^ 1],
                                    h->H, h->fft.stream.cur)

@@ -40,7 +40,7 @@ struct FirCore {
     int cur = 0;
     unsigned long long seen = 0;           // stream samples consumed (decimation phase)
     StreamSlot stream;
-    DevBuf stage_in, stage_out, stage_conv;
+    DevBuf stage_in, stage_out, stage_conv, stage_alias;
     void* os_state = nullptr;              // overlap-save plan (lazily built)
     int os_status = SDRGPU_OK;
     void* mx_state = nullptr;              // split-bf16 MFMA direct-form plan (lazily built)
@@ -76,6 +76,7 @@ struct FirCore {
         stage_in.release();
         stage_out.release();
         stage_conv.release();
+        stage_alias.release();
         if (os_state) fir_os_release(os_state);
         os_state = nullptr;
         if (mx_state) fir_mx_release(mx_state);
@@ -169,6 +170,9 @@ struct FirCore {
         if (n_out_ret) *n_out_ret = n_out;
         if (n_in == 0) return SDRGPU_OK;
         if (!d_in || (n_out > 0 && !d_out)) return SDRGPU_ERR_INVALID;
+        int st = unalias_input(stage_alias, d_in, rows_span(nch, ld_in, n_in, in_bytes()), d_out,
+                               rows_span(nch, ld_out, n_out, out_bytes()), stream.cur);
+        if (st) return st;
         FirParams p{};
         p.sample_kind = sk;
         p.tap_kind = tk;
@@ -188,7 +192,7 @@ struct FirCore {
         p.ld_out = (long)ld_out;
         p.nch = (int)nch;
         p.force_naive = 0;
-        int st = SDRGPU_ERR_UNSUPPORTED;
+        st = SDRGPU_ERR_UNSUPPORTED;
         int ran = SDRGPU_FIR_MATRIX;
         int kern = SDRGPU_FIR_KERNEL_NONE, conv = 0;
         if (want_mx()) {
