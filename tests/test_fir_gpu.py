@@ -378,6 +378,106 @@ def test_fir_mx_intra_window_dynamic_range(sdr, oracle, weak):
     assert worst <= 1e-5, f"worst 64-output window max/rms {worst:.3e} (weak {weak})"
 
 
+@pytest.mark.parametrize("sk,D", [(1, 4), (1, 2), (1, 1), (2, 4), (2, 1)])
+def test_fir_mx_silent_stretches(sdr, oracle, sk, D):
+    """Exact silence between bursts (c64 zeros; rtl_tcp byte pairs of 128, which convert to 0.0)
+    and stretches 60-230 dB apart.  Checked: (1) every output whose 255-sample window is all
+    zero is exactly 0.0, as the reference's sequential sum gives; (2) the parity bar (1e-5 of
+    the output's RMS); (3) the MFMA kernels' block-floating-point error bound, per
+    64-output window w: |y - ref| <= 1e-5 rms_w + 2^-21 max|h| sum_w|x| + 2^-38 M_tile sum|h|.
+    The second term is the taps' split / integer rounding (2^-22 of max|h|, fir_mxh.hip hh + hl,
+    fir_mxi.hip's three int8 digits); the third is the fp16 sample split under one scale per
+    1024-sample tile (fir_mxh.hip): the tile's largest sample M_tile maps to [2^14, 2^15), so a
+    sample 2^-29 below it reaches f16's subnormals and one 2^-38 below it flushes to zero.
+    A stretch 2^-39 below its neighbour in the same tile (1e-12 next to 0.5 here) is therefore
+    not resolved relative to its OWN level, unlike the reference's f32 sum -- measured, and far
+    inside (2).  The u8 path has no third term (integer samples)."""
+    from sdrgpu import _lib
+    import scipy.signal as ss
+    rng = np.random.default_rng(600 + 10 * sk + D)
+    taps = ss.firwin(255, 0.2).astype(np.float32)
+    plan = [("sig", 1.0, 5000), ("zero", 0, 1), ("sig", 1.0, 3000), ("zero", 0, 4096),
+            ("sig", 1e-3, 9000), ("zero", 0, 255), ("sig", 0.5, 2000), ("zero", 0, 70000),
+            ("sig", 1.0, 7000), ("zero", 0, 1023), ("sig", 1e-2, 30000), ("zero", 0, 3000)]
+    if sk == 1:   # c64 also gets a stretch below f16's normal range after silence
+        plan[4] = ("sig", 1e-12, 9000)
+    n = sum(p[2] for p in plan)
+    if sk == 2:
+        raw = np.full(2 * n, 128, np.uint8)
+        i = 0
+        for kind, amp, ln in plan:
+            if kind == "sig":
+                a = max(1, int(127 * amp))
+                raw[2 * i:2 * (i + ln)] = rng.integers(128 - a, 128 + a, 2 * ln).astype(np.uint8)
+            i += ln
+        x = oracle.u8_to_c64(raw)
+        inp = raw
+    else:
+        x = np.zeros(n, np.complex64)
+        i = 0
+        for kind, amp, ln in plan:
+            if kind == "sig":
+                x[i:i + ln] = (amp * (rng.standard_normal(ln) + 1j * rng.standard_normal(ln))).astype(np.complex64)
+            i += ln
+        inp = x
+    ref = oracle.Fir(taps, D, sample_kind=1).process(x)
+    f = sdr.filter.Fir(taps, decim=D, sample_kind=sk).design(2.4e6)
+    y = f.process(inp)
+    assert f.last_kernel() in (_lib.FIR_KERNEL_FP16, _lib.FIR_KERNEL_INT8), f.last_kernel()
+    assert y.shape == ref.shape
+    g = D - 1 + D * np.arange(ref.size)                   # input index of each kept output
+    nz = np.concatenate([[0], np.cumsum(x != 0)])         # nonzero inputs before index i
+    silent = nz[g + 1] - nz[np.maximum(g - 254, 0)] == 0
+    assert silent.sum() > 1000
+    assert np.all(ref[silent] == 0)
+    bad = np.nonzero(y[silent] != 0)[0]
+    assert bad.size == 0, f"{bad.size} silent outputs nonzero, first at {np.nonzero(silent)[0][bad[0]]}"
+    assert_parity(y, ref, what=f"silent stretches sk{sk} D{D}")
+    hmax, hsum, ax = float(np.abs(taps).max()), float(np.abs(taps).sum()), np.abs(x)
+    worst = (0.0, 0)
+    for w0 in range(0, ref.size - 64, 64):
+        r = ref[w0:w0 + 64]
+        g0, g1 = D - 1 + D * w0, D - 1 + D * (w0 + 63)
+        sx = float(ax[max(0, g0 - 254):g1 + 1].sum())
+        mt = float(ax[max(0, g0 - 254 - 2048):g1 + 2049].max())
+        bound = (1e-5 * np.sqrt(np.mean(np.abs(r) ** 2)) + 2.0 ** -21 * hmax * sx
+                 + (2.0 ** -38 * mt * hsum if sk == 1 else 0.0))
+        e = float(np.abs(y[w0:w0 + 64] - r).max())
+        if e > 0 and e / bound > worst[0]:
+            worst = (e / bound, w0)
+    print(f"silent sk{sk} D{D}: worst window error {worst[0]:.3f} of the bound (window {worst[1]})")
+    assert worst[0] <= 1.0, f"window {worst[1]}: error {worst[0]:.2f} x the bound"
+
+
+def test_firbank_d1_silent_channels(sdr, oracle):
+    """The D = 1 MFMA bank (configs[4]'s kernel) on 8 channels where silence, weak and strong
+    stretches fall at different offsets per channel (and two channels are silent throughout):
+    all-zero windows give exactly 0.0, every other 64-output window is within 1e-5 of its own
+    RMS."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(640)
+    nch, n, K = 8, 40000, 255
+    taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+    x = np.zeros((nch, n), np.complex64)
+    for c in range(2, nch):
+        for a0, ln, amp in ((1000 * c, 3000, 1.0), (9000 + 777 * c, 5000, 1e-4), (20000 + 313 * c, 9000, 1e3)):
+            x[c, a0:a0 + ln] = (amp * (rng.standard_normal(ln) + 1j * rng.standard_normal(ln))).astype(np.complex64)
+    b = sdr.filter.FirBank(taps, nch, sample_kind=1, decim=1)
+    y = b.process(x)
+    assert b.last_kernel() == _lib.FIR_KERNEL_FP16
+    ref = oracle.fir_batch(taps, x, 1)
+    for c in range(nch):
+        nz = np.concatenate([[0], np.cumsum(x[c] != 0)])
+        g = np.arange(n)
+        silent = nz[g + 1] - nz[np.maximum(g - K + 1, 0)] == 0
+        assert np.all(ref[c][silent] == 0) and np.all(y[c][silent] == 0), f"ch{c} silent outputs"
+        for w0 in range(0, n - 64, 64):
+            r = ref[c, w0:w0 + 64]
+            if np.any(r):
+                mx, _ = rms_rel_err(y[c, w0:w0 + 64], r)
+                assert mx <= 1e-5, f"ch{c} window {w0}: max/rms {mx:.3e}"
+
+
 @pytest.mark.parametrize("K", [1, 129, 130, 255, 257])
 def test_fir_mx_decim2_fp16_tiles(sdr, oracle, K):
     """c64 decimate-by-2 on the fp16 x 2 MFMA tiles (fir_mxh.hip at D = 2: 64-byte LDS rows with
