@@ -64,10 +64,14 @@ enum sdrgpu_fir_algo {
     SDRGPU_FIR_AUTO = 0,          /* pick per shape */
     SDRGPU_FIR_DIRECT = 1,        /* LDS-tiled direct form, register-blocked outputs */
     SDRGPU_FIR_OVERLAP_SAVE = 2,  /* polyphase overlap-save, LDS-resident FFT tiles */
-    SDRGPU_FIR_MATRIX = 3,        /* direct form on the 16-bit MFMAs with an f32-accurate operand
-                                     split: per-tile scaled fp16 x2 (decim 4, ntaps <= 257) or
-                                     exact bf16 x3 (decim 2/8); c64 samples, f32 taps, 16-B
-                                     aligned input.  AUTO picks it for those shapes. */
+    SDRGPU_FIR_MATRIX = 3,        /* direct form on the matrix cores with an f32-accurate operand
+                                     split: per-tile scaled fp16 x2 (c64, decim 1/2/4, ntaps up
+                                     to 257; rtl_tcp u8 on int8 digits) or exact bf16 x3 (c64,
+                                     decim 8); f32 taps, 16-B aligned c64 input.  AUTO picks it
+                                     for those shapes.  The fp16 split is block floating point:
+                                     a sample more than 2^29 below the largest sample of its
+                                     1024-sample tile is resolved to 2^-38 of that sample, not
+                                     to its own level (DIRECT keeps f32's range per sample). */
 };
 
 /* Which kernel ran the most recent block (sdrgpu_fir_last_kernel; test / bench introspection,
