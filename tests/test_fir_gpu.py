@@ -499,3 +499,68 @@ def test_fir_mx_decim2_fp16_tiles(sdr, oracle, K):
     yb = sdr.filter.FirBank(taps, 3, sample_kind=1, decim=2).process(xb)
     for c in range(3):
         assert_parity(yb[c], oracle.Fir(taps, 2, sample_kind=1).process(xb[c]), what=f"bank K {K} ch {c}")
+
+
+def _nonfinite_check(y, ref, what):
+    """Non-finite outputs exactly where the reference's are (NaN, and inf with its sign); the
+    finite ones within the parity bar."""
+    assert y.shape == ref.shape, what
+    for part in ("real", "imag"):
+        a, b = getattr(y, part), getattr(ref, part)
+        assert np.array_equal(np.isnan(a), np.isnan(b)), f"{what} {part}: NaN sets differ " \
+            f"({np.isnan(a).sum()} vs {np.isnan(b).sum()})"
+        assert np.array_equal(np.isposinf(a), np.isposinf(b)) and \
+            np.array_equal(np.isneginf(a), np.isneginf(b)), f"{what} {part}: inf sets differ"
+    fin = np.isfinite(ref.real) & np.isfinite(ref.imag)
+    assert_parity(y[fin], ref[fin], what=what)
+
+
+NONFINITE = [
+    # (samples index, value) groups; each case is one stream of 40000 c64 samples in two blocks
+    [(5000, complex(np.nan, 0.0))],
+    [(5003, complex(0.0, np.inf))],
+    [(0, complex(np.nan, np.nan))],                             # first sample of the stream
+    [(10239, complex(-np.inf, 1.0)), (10240, complex(np.inf, 1.0))],  # tile edge, +inf next to -inf
+    [(19999, complex(np.nan, 0.0))],                            # last sample of block 1: history
+    [(3000, complex(np.inf, 0.0)), (3100, complex(np.nan, 0.0)), (30001, complex(0.0, -np.inf))],
+]
+
+
+@pytest.mark.parametrize("D", [4, 2, 1])
+@pytest.mark.parametrize("case", range(len(NONFINITE)))
+def test_fir_mx_nonfinite_samples(sdr, oracle, D, case):
+    """inf / NaN input samples through the fp16-split MFMA kernel (fir_mxh.hip exact_tile): the
+    non-finite outputs are exactly the reference's -- the K outputs whose window holds the
+    sample (fir.rs:23-32), NaN where +inf meets -inf -- and every finite output meets the
+    parity bar; blocks carry the history (a NaN in block 1's last sample reaches block 2)."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(700 + case)
+    taps = (rng.standard_normal(255) / np.sqrt(255)).astype(np.float32)
+    n = 40000
+    x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+    for i, v in NONFINITE[case]:
+        x[i] = v
+    ref = oracle.Fir(taps, D, sample_kind=1).process(x)
+    assert not np.isfinite(ref).all()
+    f = sdr.filter.Fir(taps, decim=D, sample_kind=1).design(2.4e6)
+    y = np.concatenate([f.process(x[:20000]), f.process(x[20000:])])
+    assert f.last_kernel() == _lib.FIR_KERNEL_FP16
+    _nonfinite_check(y, ref, f"D{D} case {case}")
+
+
+def test_firbank_nonfinite_channels(sdr, oracle):
+    """The D = 1 MFMA bank with a NaN in one channel and inf in another: nothing leaks across
+    channels, and each channel's non-finite outputs are the reference's."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(720)
+    nch, n = 6, 9000
+    taps = (rng.standard_normal(255) / np.sqrt(255)).astype(np.float32)
+    x = (rng.standard_normal((nch, n)) + 1j * rng.standard_normal((nch, n))).astype(np.complex64)
+    x[1, 4000] = complex(np.nan, 0.0)
+    x[4, 1023] = complex(np.inf, -np.inf)
+    b = sdr.filter.FirBank(taps, nch, sample_kind=1, decim=1)
+    y = b.process(x)
+    assert b.last_kernel() == _lib.FIR_KERNEL_FP16
+    ref = oracle.fir_batch(taps, x, 1)
+    for c in range(nch):
+        _nonfinite_check(y[c], ref[c], f"ch{c}")

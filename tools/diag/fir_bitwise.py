@@ -4,8 +4,8 @@
     python tools/diag/fir_bitwise.py OUT_B.npz          # the product library
     python tools/diag/fir_bitwise.py --compare OUT_A.npz OUT_B.npz
 Inputs: complex noise whose block amplitude jumps over 2^-30 .. 2^30 (every per-tile scale,
-the sticky-scale cases on both sides of a power of two, the fp16-subnormal tail), plus a run
-of samples just below / above 2^k boundaries.  Cases: c64 D = 4 (255 taps, the headline
+the sticky-scale cases on both sides of a power of two, the fp16-subnormal tail, exact-zero
+stretches), plus a run of samples just below / above 2^k boundaries.  Cases: c64 D = 4 (255 taps, the headline
 kernel), D = 2, the D = 1 bank, several streamed blocks each."""
 import os
 import sys
@@ -26,6 +26,9 @@ def signal(n, seed):
     x = (x * (amp * drift)).astype(np.complex64)
     edge = rng.integers(0, n - 4096)
     x[edge:edge + 4096] = np.float32(65504.0) * np.sign(x[edge:edge + 4096].real) + 1j * np.float32(1.5)
+    # exact silence: all-zero tiles and the sticky-scale choice of the tile after them
+    for z in rng.integers(0, n - 5000, size=3):
+        x[z:z + int(rng.integers(300, 5000))] = 0
     return x
 
 

@@ -71,6 +71,10 @@ constexpr int kRunTilesU8 = 8;
 // configs[1] steady state 0.4400 -> 0.4289 ms (2 per chunk 0.4323, 8 0.4346), driver window
 // 0.501 -> 0.504 ms (noise); configs[4] bank 1.967 -> 1.954 ms in the window.
 constexpr int kStagePerChunk = 4;
+// wave_scale of a window holding inf or NaN (exact_tile below): exp2i of it is inf (that window's
+// staged values are never used), and the sticky-scale test neither keeps it into a finite window
+// nor keeps a finite scale into it
+constexpr int kNonFinite = 1 << 16;
 
 // CS: 256-output MFMA column sets per tile.  D = 1 stages the window's history once for CS
 // column sets (the history is 1.5x a 256-sample set, so re-staging it per set dominated)
@@ -207,9 +211,11 @@ __device__ __forceinline__ void put_pair(char* lds, int a, const float4& f, floa
     st32(lds, a + 3 * PLB, l);
 }
 
-// a left-leaning chain folds into two v_max3_f32 with |.| source modifiers
+// a left-leaning chain folds into two v_maximum3_f32 with |.| source modifiers: IEEE maximum,
+// so a NaN sample makes the max NaN (fmaxf / v_max3_f32 would skip it; same instruction count)
 __device__ __forceinline__ float absmax4(float m, const float4& f) {
-    return fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(f.x)), fabsf(f.y)), fabsf(f.z)), fabsf(f.w));
+    auto mx = [](float a, float b) { return __builtin_elementwise_maximum(a, b); };
+    return mx(mx(mx(mx(m, fabsf(f.x)), fabsf(f.y)), fabsf(f.z)), fabsf(f.w));
 }
 
 // window scale exponent: 15 - exponent(wave max), clamped so 2^s is a normal float.  The
@@ -234,10 +240,45 @@ __device__ __forceinline__ int wave_scale(float m) {
     // (biased 0) gives 141, clamped to 126 (round 4's v_frexp_exp form gave 15 for an exact zero:
     // an all-zero window's outputs are zero either way, but the sticky-scale keep / restage
     // choice of the odd tile after it can differ, so its low bits are not round 4's); inf / NaN
-    // (biased 255) keep frexp's 0 -> 15
+    // (biased 255; absmax4 propagates NaN) -> kNonFinite: exact_tile computes that tile
     const int e = (int)((ab > cd ? ab : cd) >> 23);
-    const int s = e == 255 ? 15 : 141 - e;
-    return s < -126 ? -126 : (s > 126 ? 126 : s);
+    const int s = 141 - e;
+    return e == 255 ? kNonFinite : (s < -126 ? -126 : (s > 126 ? 126 : s));
+}
+
+// A window holding inf or NaN (wave_scale returns kNonFinite) has no power-of-two scale, and the
+// banded Toeplitz's zero taps would carry 0 x NaN = NaN into outputs whose 255-sample window does
+// not hold the sample.  Such a tile's outputs come from the reference's own sum instead
+// (fir.rs:28-30: acc = 0; acc += x[g - k] * h[k] for k = 0 .. K-1, no FMA; convolve.rs:13-15),
+// one output per lane at a time from global memory (the tile is L2-resident), with the lanes'
+// MFMA output mapping: non-finite samples reach exactly the outputs they reach in the reference,
+// and the tile's finite outputs are bit-identical to it.  Only tiles that hold such a sample
+// take this path.
+template <int D, int CS>
+__device__ __forceinline__ void exact_tile(const MxhParams& p, long ch, int tile, int sv, int g) {
+#pragma clang fp contract(off)
+    const int K = p.K;
+    const float2* __restrict__ in = p.in + ch * p.ld_in;
+    const float2* __restrict__ hist = p.hist + ch * (long)(K - 1);
+    float2* __restrict__ out = p.out + ch * p.ld_out;
+    const long i0 = D - 1 - p.delta;
+#pragma unroll 1
+    for (int o = 0; o < 4 * CS; ++o) {  // column set o / 4, output o % 4 of the lane's four
+        {
+            const long m = (long)tile * (256 * CS) + 256 * (o >> 2) + 16 * sv + 4 * g + (o & 3);
+            if (m >= p.n_out) continue;
+            const long gi = i0 + (long)D * m;
+            float ar = 0.f, ai = 0.f;
+#pragma unroll 1
+            for (int k = 0; k < K; ++k) {
+                const float2 xv = fetch1(in, hist, gi - k, p.n_in, K);
+                const float hk = p.taps[k];
+                ar += xv.x * hk;
+                ai += xv.y * hk;
+            }
+            out[m] = make_float2(ar, ai);
+        }
+    }
 }
 
 __device__ __forceinline__ float exp2i(int s) { return __builtin_amdgcn_ldexpf(1.0f, s); }
@@ -580,36 +621,40 @@ void fir_mxh_kernel(MxhParams p) {
             if (!fast2 && ld.ok) load_tile(nx, ld);
             const int so = -(s_cur + p.sh);
             const int tile = cm.tu + cm.t;
-            float2* __restrict__ out = p.out + cm.ch * p.ld_out;
-            // the tile's output base is scalar; the lanes' byte offsets inside it are fixed
-            char* __restrict__ outt = reinterpret_cast<char*>(out + (long)tile * G::TO);
+            if (!U8 && s_cur == kNonFinite) {
+                exact_tile<D, CS>(p, cm.ch, tile, sv, g);
+            } else {
+                float2* __restrict__ out = p.out + cm.ch * p.ld_out;
+                // the tile's output base is scalar; the lanes' byte offsets inside it are fixed
+                char* __restrict__ outt = reinterpret_cast<char*>(out + (long)tile * G::TO);
 #pragma unroll
-            for (int j = 0; j < CS; ++j) {
-                float yr[4], yi[4];
+                for (int j = 0; j < CS; ++j) {
+                    float yr[4], yi[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
-                    yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
-                }
-                if (p.vec_out && tile * CS + j < p.oblk) {
-                    // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
-                    // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
-                    // line) and the second those of the odd-v blocks (steady-state probe: 0.472
-                    // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
-                    const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
-                    const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
-                    f32x4 rx;
+                    for (int i = 0; i < 4; ++i) {
+                        yr[i] = __builtin_amdgcn_ldexpf(cr[j][i], so);
+                        yi[i] = __builtin_amdgcn_ldexpf(ci[j][i], so);
+                    }
+                    if (p.vec_out && tile * CS + j < p.oblk) {
+                        // line-complete stores: lanes v and v^1 (same g) swap one 16-B half, so the
+                        // first store writes the 128-B lines of the even-v blocks whole (8 lanes per
+                        // line) and the second those of the odd-v blocks (steady-state probe: 0.472
+                        // vs 0.487 ms for half-line pairs, profiles/r03s3_stream_probe3.txt)
+                        const f32x4 y0 = {yr[0], yi[0], yr[1], yi[1]};
+                        const f32x4 y1 = {yr[2], yi[2], yr[3], yi[3]};
+                        f32x4 rx;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
-                            __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
-                    __builtin_nontemporal_store(ev ? y0 : rx, reinterpret_cast<f32x4*>(outt + (ob1 + 2048u * j)));
-                    __builtin_nontemporal_store(ev ? rx : y1, reinterpret_cast<f32x4*>(outt + (ob2 + 2048u * j)));
-                } else {
-                    const long m = (long)tile * G::TO + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
+                        for (int q = 0; q < 4; ++q)
+                            rx[q] = __int_as_float(__builtin_amdgcn_mov_dpp(
+                                __float_as_int(ev ? y1[q] : y0[q]), 0xB1, 0xf, 0xf, false));
+                        __builtin_nontemporal_store(ev ? y0 : rx, reinterpret_cast<f32x4*>(outt + (ob1 + 2048u * j)));
+                        __builtin_nontemporal_store(ev ? rx : y1, reinterpret_cast<f32x4*>(outt + (ob2 + 2048u * j)));
+                    } else {
+                        const long m = (long)tile * G::TO + 256 * j + 16 * sv + 4 * g;  // sv = block of column v
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+                        for (int i = 0; i < 4; ++i)
+                            if (m + i < p.n_out) out[m + i] = make_float2(yr[i], yi[i]);
+                    }
                 }
             }
             s_cur = s_next;
