@@ -564,3 +564,55 @@ def test_firbank_nonfinite_channels(sdr, oracle):
     ref = oracle.fir_batch(taps, x, 1)
     for c in range(nch):
         _nonfinite_check(y[c], ref[c], f"ch{c}")
+
+
+NONFINITE_PATHS = [
+    # (sample kind, tap kind, ntaps, decim, algorithm, expected kernel)
+    (0, 0, 127, 1, "auto", "direct"),      # configs[0]'s shape: the R-blocked direct kernel
+    (1, 0, 255, 1, "direct", "direct"),    # fir_direct2 (wave-private, D = 1)
+    (1, 0, 255, 4, "direct", "direct"),    # fir_direct4 (D = 4)
+    (1, 0, 255, 2, "direct", "direct"),    # fir_direct4 (D = 2)
+    (1, 1, 63, 3, "auto", "direct"),       # complex taps, D = 3: the R-blocked direct kernel
+    (1, 0, 255, 4, "os", "os"),            # overlap-save, persistent form (D = 4)
+    (1, 0, 255, 1, "os", "os"),            # overlap-save, D = 1
+    (1, 1, 255, 2, "auto", "os"),          # complex taps: AUTO takes overlap-save
+    (1, 0, 255, 8, "auto", "bf16x3"),      # D = 8: the exact bf16 x3 MFMA kernel
+    (1, 0, 33, 64, "auto", "direct"),      # very large D: the naive kernel
+]
+
+
+@pytest.mark.parametrize("path", NONFINITE_PATHS, ids=lambda c: "sk{}tk{}K{}D{}{}".format(*c[:5]))
+def test_fir_nonfinite_samples_every_path(sdr, oracle, path):
+    """inf / NaN samples through every other FIR kernel: padded taps, FFT blocks and the bf16x3
+    Toeplitz would carry one beyond the outputs whose window holds it; non-finite outputs are
+    replaced by the reference's sum (fir_exact.hpp), so the non-finite sets are the
+    reference's and the finite outputs meet the parity bar, over two streamed blocks."""
+    from sdrgpu import _lib
+    sk, tk, K, D, algo, kern = path
+    rng = np.random.default_rng(800 + K + D)
+    taps = (rng.standard_normal(K) / np.sqrt(K)).astype(np.float32)
+    if tk == 1:
+        taps = (taps + 1j * rng.standard_normal(K) / np.sqrt(K)).astype(np.complex64)
+    n = 60000
+    if sk == 0:
+        x = rng.standard_normal(n).astype(np.float32)
+        marks = [(100, np.nan), (20000, np.inf), (29999, -np.inf), (45000, np.nan), (45001, np.inf)]
+    else:
+        x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+        marks = [(100, complex(np.nan, 0)), (20000, complex(0, np.inf)), (29999, complex(-np.inf, 1)),
+                 (45000, complex(np.nan, np.nan)), (45001, complex(np.inf, -np.inf))]
+    for i, v in marks:
+        x[i] = v
+    ref = oracle.Fir(taps, D, sample_kind=sk).process(x)
+    f = fir(sdr, taps, sk, D, algo)
+    y = np.concatenate([f.process(x[:30000]), f.process(x[30000:])])
+    want = {"direct": _lib.FIR_KERNEL_DIRECT, "os": _lib.FIR_KERNEL_OVERLAP_SAVE,
+            "bf16x3": _lib.FIR_KERNEL_BF16X3}[kern]
+    assert f.last_kernel() == want, (f.last_kernel(), want)
+    if sk == 0:
+        assert np.array_equal(np.isnan(y), np.isnan(ref))
+        assert np.array_equal(np.isposinf(y), np.isposinf(ref)) and np.array_equal(np.isneginf(y), np.isneginf(ref))
+        fin = np.isfinite(ref)
+        assert_parity(y[fin], ref[fin], what=str(path))
+    else:
+        _nonfinite_check(y, ref, str(path))

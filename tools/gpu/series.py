@@ -12,7 +12,10 @@ Phases (one JSON line each, per-launch ms in "ms"):
   idle     1 s host sleep (GPU idle), then 60 launches
 --kind: c64 = configs[1] (the headline), u8 = configs[1] fed from rtl_tcp u8 (bench_configs
 c2u8), bank = configs[4]'s 8192-channel D = 1 bank (bench.py's channel-sharded leg), u8dN =
-2^26 rtl_tcp u8 samples through the 255-tap FIR at decimation N (1, 2, 8).
+2^26 rtl_tcp u8 samples through the 255-tap FIR at decimation N (1, 2, 8); c64d2 / c64d8 = 2^26
+c64 samples at decimation 2 / 8, c64dir4 / c64dir1 / c64os4 = the same forced onto the VALU
+direct form (D = 4 / 1) or overlap-save (D = 4); f32d1 = configs[0]'s 127-tap real filter over
+2^26 f32 samples.
 --clk: the library is tools/experiments/fir_ablate.sh's `clk` variant, which writes per
 workgroup (100 MHz ticks, shader-clock ticks) over the launch 4 KiB before its output
 pointer; each launch gets its own output offset so the records survive, and every phase
@@ -38,7 +41,8 @@ GUARD = 1024  # c64 elements (8 KiB) of output offset per launch under --clk
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1", "u8d2", "u8d8", "c64d2"])
+    ap.add_argument("--kind", default="c64", choices=["c64", "u8", "bank", "u8d1", "u8d2", "u8d8", "c64d2",
+                                                      "c64d8", "c64dir4", "c64dir1", "c64os4", "f32d1"])
     ap.add_argument("--clk", action="store_true")
     ap.add_argument("--long", type=int, default=300)
     args = ap.parse_args()
@@ -62,19 +66,36 @@ def main():
 
         def launch(i):
             f.process_dev(x.ptr, n, n, y.ptr + 8 * guard * (i + 1), n)
-    elif args.kind == "c64d2":  # 2^26 c64 samples, decimation 2 (8 B in + 4 B out per sample)
+    elif args.kind in ("c64d2", "c64d8", "c64dir4", "c64dir1", "c64os4"):
+        # 2^26 c64 samples: decimation 2 / 8 (AUTO), or D = 4 / 1 forced onto the VALU direct
+        # form / D = 4 onto overlap-save (the secondary paths)
         n = 1 << 26
-        dec = 2
-        f = sdrgpu.filter.Fir(taps, decim=2, sample_kind=_lib.C64).design(2.4e6)
+        dec = {"c64d2": 2, "c64d8": 8, "c64dir4": 4, "c64dir1": 1, "c64os4": 4}[args.kind]
+        algo = {"c64dir4": _lib.FIR_DIRECT, "c64dir1": _lib.FIR_DIRECT,
+                "c64os4": _lib.FIR_OVERLAP_SAVE}.get(args.kind, _lib.FIR_AUTO)
+        f = sdrgpu.filter.Fir(taps, decim=dec, sample_kind=_lib.C64, algorithm=algo).design(2.4e6)
         pat = bench.synth_iq_pattern(1 << 22, seed=1000)
         x = DeviceBuffer.empty(n, np.complex64)
         for off in range(0, n, pat.size):
             x.upload(pat[:min(pat.size, n - off)], offset_bytes=8 * off)
-        out_n = n // 2
+        out_n = n // dec
         y = DeviceBuffer.empty(out_n + guard * (nlaunch + 1), np.complex64)
 
         def launch(i):
             f.process_dev(x.ptr, n, y.ptr + 8 * guard * (i + 1), out_n)
+    elif args.kind == "f32d1":  # configs[0]'s filter (127 real taps) over 2^26 f32 samples
+        n = 1 << 26
+        f = sdrgpu.filter.Fir(ss.firwin(127, 0.2).astype(np.float32), decim=1,
+                              sample_kind=_lib.F32).design(2.4e6)
+        x = DeviceBuffer.empty(n, np.float32)
+        pat = np.random.default_rng(22).standard_normal(1 << 22).astype(np.float32)
+        for off in range(0, n, pat.size):
+            x.upload(pat[:min(pat.size, n - off)], offset_bytes=4 * off)
+        out_n = n
+        y = DeviceBuffer.empty(out_n + guard * (nlaunch + 1), np.float32)
+
+        def launch(i):
+            f.process_dev(x.ptr, n, y.ptr + 4 * guard * (i + 1), out_n)
     elif args.kind.startswith("u8d"):  # u8 stream, decimation 1 / 2 / 8: 2 B in + 8/D B out per sample
         n = 1 << 26
         dec = int(args.kind[3:])

@@ -18,7 +18,7 @@
 // c64 it is FP32-VALU bound, see DESIGN.md.
 #include <cstdlib>
 
-#include "fir_kernels.hpp"
+#include "fir_exact.hpp"
 
 namespace sdrgpu {
 
@@ -107,8 +107,8 @@ __global__ __launch_bounds__(kBlock) void fir_direct_kernel(FirParams p) {
         }
         const long mq = m0 + (long)tid * R;
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (mq + r < p.n_out) out[mq + r] = acc[r];
+        for (int r = 0; r < R; ++r)  // non-finite outputs: the reference's sum (fir_exact.hpp)
+            if (mq + r < p.n_out) out[mq + r] = fir_checked<TS, TT>(p, in, hist, mq + r, acc[r]);
     }
 
     if (blockIdx.x == gridDim.x - 1) {

@@ -26,7 +26,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "fir_kernels.hpp"
+#include "fir_exact.hpp"
 
 namespace sdrgpu {
 
@@ -164,7 +164,16 @@ __global__ __launch_bounds__(kD2Block, 2) void fir_direct2_kernel(FirParams p, l
         // ---- kept outputs: lane writes R consecutive samples ----
         const long m = tile * TO + (long)R * lane;
         float2* o = out + m;
-        if (m + R <= p.n_out) {
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < R; ++j) bad |= !all_finite(acc[j]);
+        if (bad) {
+            // an inf / NaN sample in the lane's reach: its outputs from the reference's sum
+            // (the zero-padded taps would carry it further; fir_exact.hpp)
+#pragma unroll 1
+            for (int j = 0; j < R; ++j)
+                if (m + j < p.n_out) o[j] = fir_exact_output<float2, float>(p, in, hist, m + j);
+        } else if (m + R <= p.n_out) {
 #pragma unroll
             for (int j = 0; j < R; ++j) o[j] = acc[j];
         } else {
@@ -345,7 +354,16 @@ __global__ __launch_bounds__(kD2Block, 2) void fir_direct4_kernel(FirParams p, l
 
         const long m = tile * TO + (long)R * lane;
         float2* o = out + m;
-        if (m + R <= p.n_out) {
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < R; ++j) bad |= !all_finite(acc[j]);
+        if (bad) {
+            // an inf / NaN sample in the lane's reach: its outputs from the reference's sum
+            // (the zero-padded taps would carry it further; fir_exact.hpp)
+#pragma unroll 1
+            for (int j = 0; j < R; ++j)
+                if (m + j < p.n_out) o[j] = fir_exact_output<float2, float>(p, in, hist, m + j);
+        } else if (m + R <= p.n_out) {
 #pragma unroll
             for (int j = 0; j < R; j += 2)
                 *reinterpret_cast<f4u*>(o + j) = f4u{acc[j].x, acc[j].y, acc[j + 1].x, acc[j + 1].y};

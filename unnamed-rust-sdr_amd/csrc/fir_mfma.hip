@@ -36,7 +36,7 @@
 #include <cmath>
 #include <cstdlib>
 
-#include "fir_kernels.hpp"
+#include "fir_exact.hpp"
 #include "fir_mxi.hpp"
 
 namespace sdrgpu {
@@ -64,7 +64,31 @@ struct MxParams {
     float2* out;
     long ld_out;
     int n_iter;          // iterations per segment (multiple of NACC)
+    int D, tpp;          // for fir_exact_output (polyphase taps_pm)
+    const void* taps_pm;
 };
+
+// A non-finite MFMA output came from an inf / NaN sample in its step's window, which the zero
+// taps of the Toeplitz carry to all 16 outputs of the step.  The main loop only notes that a lane
+// stored one (its registers are full); afterwards the lane re-reads its own outputs (rows 4g + i,
+// column v of every step: same-thread read-after-write) and replaces the non-finite ones with
+// the reference's sum (fir_exact.hpp).
+__device__ __forceinline__ void mx_exact_fixup(const MxParams& p, long wave, int g, int v) {
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        const long sg = wave * 16 + 4 * g + i;
+        if (sg >= p.nseg) break;
+        const long ch = sg / p.nseg_ch;
+        const long m = (sg - ch * p.nseg_ch) * p.seg_len;
+        const long rem = p.n_out - m, lim = rem < p.seg_len ? rem : p.seg_len;
+        float2* __restrict__ out = p.out + ch * p.ld_out + m;
+#pragma unroll 1
+        for (long o = v; o < lim; o += 16)
+            if (!all_finite(out[o]))
+                out[o] = fir_exact_output<float2, float>(p, p.in + ch * p.ld_in,
+                                                         p.hist + ch * (long)(p.K - 1), m + o);
+    }
+}
 
 // Split a pair of floats into three packed bf16 pairs (a -> low half, b -> high half):
 // hi = top 16 bits, mid = top 16 bits of the exact remainder, lo = the rest (exact).
@@ -187,6 +211,7 @@ void fir_mx_kernel(MxParams p) {
         acci[a] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     float4 raw[NACC][NP];
+    bool nonfinite = false;    // this lane stored a non-finite output (mx_exact_fixup)
     const long hop = 16L * D;  // input samples per step
 #pragma unroll
     for (int r = 0; r < NACC; ++r)
@@ -249,13 +274,16 @@ void fir_mx_kernel(MxParams p) {
             if (t >= 0) {
                 const long o = 16 * t;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i) {
+                    nonfinite |= !all_finite(make_float2(accr[slot][i], acci[slot][i]));
                     if (o + v < lim[i]) outp[i][o] = make_float2(accr[slot][i], acci[slot][i]);
+                }
             }
             accr[slot] = f32x4{0.f, 0.f, 0.f, 0.f};
             acci[slot] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
+    if (nonfinite) mx_exact_fixup(p, wave, g, v);
 
     if (p.hist_next) {  // stream history carry, spread over the whole grid
         const long nch = (p.nseg + p.nseg_ch - 1) / p.nseg_ch;
@@ -389,6 +417,9 @@ int fir_mx_launch(const FirParams& fp, void* state, hipStream_t s, int* kernel) 
     p.delta = (int)((fp.i0 + 1) & 1);
     p.out = static_cast<float2*>(fp.out);
     p.ld_out = fp.ld_out;
+    p.D = D;
+    p.tpp = fp.tpp;
+    p.taps_pm = fp.taps_pm;
     // segments: one wave per SIMD chip-wide, 16 segments per wave
     const long target = 16L * 4 * st->cus;
     const long total = fp.n_out * (long)fp.nch;

@@ -32,7 +32,7 @@
 #include <vector>
 
 #include "fft_device.hpp"
-#include "fir_kernels.hpp"
+#include "fir_exact.hpp"
 
 namespace sdrgpu {
 
@@ -57,7 +57,26 @@ struct OsParams {
     const float2* tw;            // exp(-2 pi i m / 4096), m < 4096
     float2* out;
     long ld_out;
+    int D, tpp, tap_c64;  // for fir_exact_output
+    const void* taps_pm;
 };
+
+// an FFT block mixes every sample it holds, so one inf / NaN makes all of its outputs
+// non-finite; a lane holding such outputs stores the reference's sum for them instead
+// (fir_exact.hpp), outputs m0 + stride * r, r < n (those with ok(r))
+template <typename OK>
+__device__ __forceinline__ void os_exact(const OsParams& p, const float2* __restrict__ in,
+                                                 const float2* __restrict__ hist,
+                                                 float2* __restrict__ out, long m0, int stride,
+                                                 int n, OK ok) {
+#pragma unroll 1
+    for (int r = 0; r < n; ++r) {
+        const long m = m0 + (long)stride * r;
+        if (!ok(r) || m >= p.n_out) continue;
+        out[m] = p.tap_c64 ? fir_exact_output<float2, float2>(p, in, hist, m)
+                           : fir_exact_output<float2, float>(p, in, hist, m);
+    }
+}
 
 template <int D>
 __global__ __launch_bounds__(kOsBlock) void fir_os_kernel(OsParams p) {
@@ -186,11 +205,18 @@ __global__ __launch_bounds__(kOsBlock) void fir_os_kernel(OsParams p) {
             twiddle<16, true>(v, tw, j * D);
             Dft<16, true>::run(v);
             const int skip = L - p.M;  // circular-wrap outputs
+            bool bad = false;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = j + NBI * r;
-                const long m = m0 + (i - skip);
-                if (i >= skip && m < p.n_out) out[m] = v[r];
+            for (int r = 0; r < 16; ++r) bad |= !all_finite(v[r]);
+            if (bad) {
+                os_exact(p, in, hist, out, m0 + j - skip, NBI, 16, [&](int r) { return j + NBI * r >= skip; });
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = j + NBI * r;
+                    const long m = m0 + (i - skip);
+                    if (i >= skip && m < p.n_out) out[m] = v[r];
+                }
             }
         }
     }
@@ -397,10 +423,14 @@ __global__ __launch_bounds__(kOsBlock, W) void fir_os2_kernel(OsParams p, long n
             dft4<true>(a0, a1, a2, a3);
             const long m0 = q * p.M - skip + j;
             float2* o = out + m0;
-            if (j >= skip && m0 < p.n_out) o[0] = a0;
-            if (j + NI >= skip && m0 + NI < p.n_out) o[NI] = a1;
-            if (j + 2 * NI >= skip && m0 + 2 * NI < p.n_out) o[2 * NI] = a2;
-            if (j + 3 * NI >= skip && m0 + 3 * NI < p.n_out) o[3 * NI] = a3;
+            if (!((int)all_finite(a0) & (int)all_finite(a1) & (int)all_finite(a2) & (int)all_finite(a3))) {
+                os_exact(p, in, hist, out, m0, NI, 4, [&](int r) { return j + NI * r >= skip; });
+            } else {
+                if (j >= skip && m0 < p.n_out) o[0] = a0;
+                if (j + NI >= skip && m0 + NI < p.n_out) o[NI] = a1;
+                if (j + 2 * NI >= skip && m0 + 2 * NI < p.n_out) o[2 * NI] = a2;
+                if (j + 3 * NI >= skip && m0 + 3 * NI < p.n_out) o[3 * NI] = a3;
+            }
         }
         __syncthreads();  // I5 reads of bufB finish before the next P1 writes
     }
@@ -515,6 +545,10 @@ int fir_os_launch(const FirParams& fp, void* os_state, hipStream_t s) {
     p.tw = st->d_tw;
     p.out = static_cast<float2*>(fp.out);
     p.ld_out = fp.ld_out;
+    p.D = fp.D;
+    p.tpp = fp.tpp;
+    p.tap_c64 = fp.tap_kind == SDRGPU_C64;
+    p.taps_pm = fp.taps_pm;
     const long nblk = fp.n_out > 0 ? ceil_div(fp.n_out, st->M) : 1;
     dim3 grid((unsigned)nblk, (unsigned)fp.nch);
     // D = 4 | 8: persistent workgroups (4 per CU) with the branch spectra in registers; the
