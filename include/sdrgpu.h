@@ -125,7 +125,9 @@ int sdrgpu_event_destroy(void* event);
  * decim D > 1 only outputs at stream indices D-1, 2D-1, ... are produced (the reference
  * computes all and Decimate drops D-1 of every D; only the kept ones are computed here).
  * State (ntaps-1 history, decimation phase) carries across process() calls, so any
- * partition of a stream into blocks gives the same outputs.
+ * partition of a stream into blocks gives the same outputs.  An inf / NaN sample makes
+ * exactly the outputs non-finite whose ntaps-sample window holds it, as in the reference
+ * (every algorithm recomputes such outputs with the reference's sequential sum).
  * Kinds: (F32,F32), (C64,F32), (C64,C64), and (CU8,F32), (CU8,C64) for rtl_tcp u8 IQ
  * (the reference's rtl.listen().filter(...) chain, examples/live.rs:29-31, src/main.rs:38-49):
  * the (v-128)/128 conversion is fused into the FIR load (decim 4 with f32 taps runs on the
