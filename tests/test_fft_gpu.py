@@ -144,8 +144,11 @@ def test_rfft_14400_packed_batch_and_unaligned(sdr):
 
 
 @pytest.mark.parametrize("n,hop", [(1000, 400), (1000, 1000), (1001, 333), (14400, 7200),
-                                   (4099, 2048)])
+                                   (4099, 2048), (64, 100), (1000, 2500), (4096, 5000), (16, 1),
+                                   (65536, 70000)])
 def test_stft_any_size_streaming(sdr, oracle, n, hop):
+    """Window(n) + Decimate(hop) streamed in ragged blocks (adapters/mod.rs:270-303), including
+    hops longer than the frame (frames skip samples) and hop = 1 (a frame per sample)."""
     rng = np.random.default_rng(n * 3 + hop)
     total = hop * 7 + 55
     x = cplx(rng, total)
