@@ -7,7 +7,10 @@ instruction pair (profiles/r06_hazard.txt).  Both sides claim the
     allocate all 512 VGPRs (incl. AGPRs) of their SIMD;
   * the two-waves-per-SIMD MFMA FIR kernels (fir_mxh_kernel, fir_mxi_kernel) allocate 256 VGPRs
     and no AGPRs each, so the pair fills the SIMD.
-Reads the amdhsa kernel metadata of libsdrgpu.so's gfx950 code objects with the ROCm LLVM tools."""
+And the two-wave MFMA kernels themselves carry no packed-f32 result read by the next instruction
+without a wait state (the same fault inside fir_mxh, round 6: profiles/r06_pkfault.txt).
+Reads the amdhsa kernel metadata and disassembly of libsdrgpu.so's gfx950 code objects with the
+ROCm LLVM tools."""
 import os
 import re
 import struct
@@ -84,3 +87,69 @@ def test_mfma_fir_kernels_fill_their_simd(tmp_path):
     assert not bad, f"two-wave MFMA FIR kernels that leave room on their SIMD: {bad}"
     bad = {k: v for k, v in one.items() if v[0] < 512}
     assert not bad, f"one-wave MFMA FIR kernels that leave room on their SIMD: {bad}"
+
+
+def code_objects(tmp_path):
+    """Paths of the gfx950 code objects bundled in libsdrgpu.so's .hip_fatbin."""
+    sec = tmp_path / "fatbin2"
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={sec}", LIB,
+                    str(tmp_path / "copy2.so")], check=True)
+    data = sec.read_bytes()
+    out, pos = [], 0
+    while (i := data.find(MAGIC, pos)) >= 0:
+        n = struct.unpack_from("<Q", data, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tl].decode()
+            p += 24 + tl
+            if "gfx950" in triple and size:
+                co = tmp_path / f"co{len(out)}.o"
+                co.write_bytes(data[i + off:i + off + size])
+                out.append(co)
+        pos = i + len(MAGIC)
+    return out
+
+
+@NEEDS_LIB
+def test_two_wave_mfma_kernels_have_no_uncovered_packed_f32_pairs(tmp_path):
+    """a v_pk_*_f32 result read by the very next VALU instruction with no wait
+    state in between (the compiler leaves none when the producer's op_sel_hi[0] is 0) came out
+    wrong in lanes 48-63 while another wave's MFMAs ran on the SIMD -- in the PLL beside bank
+    waves, and in fir_mxh's own inf / NaN sums beside its partner wave.  The kernels that run two
+    waves per SIMD next to MFMAs (fir_mxh, fir_mxi) must contain no such pair; their covered
+    pairs (an s_nop between) are counted too, so a new one shows up here."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
+    import pk_hazard_edit as pk
+    lines, names = [], []
+    for co in code_objects(tmp_path):
+        blob = co.read_bytes()
+        if b"fir_mxh_kernel" not in blob and b"fir_mxi_kernel" not in blob:
+            continue  # only the translation units that hold the two-wave MFMA kernels
+        syms = sorted(set(re.findall(rb"_ZN6sdrgpu12_GLOBAL__N_114fir_mx[hi]_kernelI\w+", blob)))
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn",
+                              "--disassemble-symbols=" + ",".join(x.decode() for x in syms), str(co)],
+                             capture_output=True, text=True, check=True).stdout
+        cur = None
+        for raw in dis.split("\n"):
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:", raw)
+            if m:
+                cur = m.group(1)
+                lines.append(cur + ":")
+                names.append(cur)
+                continue
+            lines.append(raw.split("//")[0].rstrip())
+            names.append(cur)
+    pairs = pk.pairs(lines)
+    two_wave = re.compile(r"(fir_mxh_kernel|fir_mxi_kernel)I")
+    seen = {n for n in names if n and two_wave.search(n)}
+    assert len(seen) >= 14, sorted(seen)
+    uncovered = [(names[a], lines[a].strip()) for a, _, cov, _ in pairs
+                 if not cov and names[a] and two_wave.search(names[a])]
+    assert not uncovered, f"uncovered packed-f32 pairs in two-wave MFMA kernels: {uncovered[:4]}"
+    covered = [names[a] for a, _, cov, _ in pairs if cov and names[a] and two_wave.search(names[a])]
+    # fir_mxi's output combination (2^16 C2 + 2^8 C1 + C0) 2^-s: 14 pairs, each behind the
+    # compiler's s_nop 0 (never seen to fail); fir_mxh: none
+    assert not any("fir_mxh_kernel" in n for n in covered), covered
+    assert len(covered) <= 14, len(covered)

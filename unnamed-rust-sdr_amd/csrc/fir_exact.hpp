@@ -35,6 +35,7 @@ __device__ __forceinline__ void exact_add(c64& a, c64 b) {
     a.x += b.x;
     a.y += b.y;
 }
+constexpr int kExactBatch = 8;
 // P: FirParams, or a kernel's own parameter block with the same i0 / n_in / K / D / taps_pm / tpp
 template <typename TS, typename TT, typename P>
 __device__ __forceinline__ TS fir_exact_output(const P& p, const TS* __restrict__ in,
@@ -42,6 +43,28 @@ __device__ __forceinline__ TS fir_exact_output(const P& p, const TS* __restrict_
     const TT* __restrict__ taps = static_cast<const TT*>(p.taps_pm);
     const long g = p.i0 + m * p.D;
     TS acc = zero_of<TS>();
+    if (g - (p.K - 1) >= 0 && g < p.n_in) {
+        // window inside this block: kExactBatch loads in flight per step, the sum still in k
+        // order (an all-NaN stream takes this path for every output)
+        const TS* __restrict__ xp = in + g;
+        const int kb = p.K - p.K % kExactBatch;
+#pragma unroll 1
+        for (int k = 0; k < kb; k += kExactBatch) {
+            TS xv[kExactBatch];
+            TT hk[kExactBatch];
+#pragma unroll
+            for (int u = 0; u < kExactBatch; ++u) {
+                xv[u] = xp[-(k + u)];
+                hk[u] = taps[(long)((k + u) % p.D) * p.tpp + (k + u) / p.D];
+            }
+#pragma unroll
+            for (int u = 0; u < kExactBatch; ++u) exact_add(acc, exact_prod(xv[u], hk[u]));
+        }
+#pragma unroll 1
+        for (int k = kb; k < p.K; ++k)
+            exact_add(acc, exact_prod(xp[-k], taps[(long)(k % p.D) * p.tpp + k / p.D]));
+        return acc;
+    }
 #pragma unroll 1
     for (int k = 0; k < p.K; ++k) {
         const long j = g - k;

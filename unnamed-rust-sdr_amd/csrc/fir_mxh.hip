@@ -254,6 +254,18 @@ __device__ __forceinline__ int wave_scale(float m) {
 // MFMA output mapping: non-finite samples reach exactly the outputs they reach in the reference,
 // and the tile's finite outputs are bit-identical to it.  Only tiles that hold such a sample
 // take this path.
+// One f32 multiply-then-add per call, as the VOP2 instructions: the compiler would otherwise pair
+// the re and im chains into v_pk_mul_f32 / v_pk_add_f32, and packed-f32 results read by the next
+// packed op came out wrong (the low half, in 16-lane groups, run to run) in this wave while its
+// SIMD partner ran MFMAs -- the fault of DESIGN.md 3.6, reproduced inside this kernel
+// (profiles/r06_nonfinite.txt).  IEEE-exact, no contraction: the reference's `acc += x * h`.
+__device__ __forceinline__ float mul_add_vop2(float acc, float x, float h) {
+    float p, r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(p) : "v"(x), "v"(h));
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(acc), "v"(p));
+    return r;
+}
+
 template <int D, int CS>
 __device__ __forceinline__ void exact_tile(const MxhParams& p, long ch, int tile, int sv, int g) {
 #pragma clang fp contract(off)
@@ -269,12 +281,41 @@ __device__ __forceinline__ void exact_tile(const MxhParams& p, long ch, int tile
             if (m >= p.n_out) continue;
             const long gi = i0 + (long)D * m;
             float ar = 0.f, ai = 0.f;
+            if (gi - (K - 1) >= 0 && gi < p.n_in) {
+                // window inside this block: 16 loads in flight per step, the sum still in k order
+                // (an all-NaN stream takes this path in every tile)
+                const float2* __restrict__ xp = in + gi;
+                const int kb = K & ~15;
 #pragma unroll 1
-            for (int k = 0; k < K; ++k) {
-                const float2 xv = fetch1(in, hist, gi - k, p.n_in, K);
-                const float hk = p.taps[k];
-                ar += xv.x * hk;
-                ai += xv.y * hk;
+                for (int k = 0; k < kb; k += 16) {
+                    float2 xv[16];
+                    float hk[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        xv[u] = xp[-(k + u)];
+                        hk[u] = p.taps[k + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        ar = mul_add_vop2(ar, xv[u].x, hk[u]);
+                        ai = mul_add_vop2(ai, xv[u].y, hk[u]);
+                    }
+                }
+#pragma unroll 1
+                for (int k = kb; k < K; ++k) {
+                    const float2 xv = xp[-k];
+                    const float hk = p.taps[k];
+                    ar = mul_add_vop2(ar, xv.x, hk);
+                    ai = mul_add_vop2(ai, xv.y, hk);
+                }
+            } else {
+#pragma unroll 1
+                for (int k = 0; k < K; ++k) {
+                    const float2 xv = fetch1(in, hist, gi - k, p.n_in, K);
+                    const float hk = p.taps[k];
+                    ar = mul_add_vop2(ar, xv.x, hk);
+                    ai = mul_add_vop2(ai, xv.y, hk);
+                }
             }
             out[m] = make_float2(ar, ai);
         }
