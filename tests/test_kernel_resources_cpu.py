@@ -116,8 +116,8 @@ def test_two_wave_mfma_kernels_have_no_uncovered_packed_f32_pairs(tmp_path):
     """a v_pk_*_f32 result read by the very next VALU instruction with no wait
     state in between (the compiler leaves none when the producer's op_sel_hi[0] is 0) came out
     wrong in lanes 48-63 while another wave's MFMAs ran on the SIMD -- in the PLL beside bank
-    waves, and in fir_mxh's own inf / NaN sums beside its partner wave.  The kernels that run two
-    waves per SIMD next to MFMAs (fir_mxh, fir_mxi) must contain no such pair; their covered
+    waves, and in fir_mxh's own inf / NaN sums beside its partner wave.  The MFMA FIR kernels
+    (fir_mxh and fir_mxi, two waves per SIMD; fir_mx) must contain no such pair; their covered
     pairs (an s_nop between) are counted too, so a new one shows up here."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tools", "diag"))
@@ -125,9 +125,9 @@ def test_two_wave_mfma_kernels_have_no_uncovered_packed_f32_pairs(tmp_path):
     lines, names = [], []
     for co in code_objects(tmp_path):
         blob = co.read_bytes()
-        if b"fir_mxh_kernel" not in blob and b"fir_mxi_kernel" not in blob:
-            continue  # only the translation units that hold the two-wave MFMA kernels
-        syms = sorted(set(re.findall(rb"_ZN6sdrgpu12_GLOBAL__N_114fir_mx[hi]_kernelI\w+", blob)))
+        if b"fir_mxh_kernel" not in blob and b"fir_mxi_kernel" not in blob and b"fir_mx_kernel" not in blob:
+            continue  # only the translation units that hold the MFMA FIR kernels
+        syms = sorted(set(re.findall(rb"_ZN6sdrgpu12_GLOBAL__N_11[34]fir_mx[hi]?_kernelI\w+", blob)))
         dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn",
                               "--disassemble-symbols=" + ",".join(x.decode() for x in syms), str(co)],
                              capture_output=True, text=True, check=True).stdout
@@ -142,12 +142,12 @@ def test_two_wave_mfma_kernels_have_no_uncovered_packed_f32_pairs(tmp_path):
             lines.append(raw.split("//")[0].rstrip())
             names.append(cur)
     pairs = pk.pairs(lines)
-    two_wave = re.compile(r"(fir_mxh_kernel|fir_mxi_kernel)I")
+    two_wave = re.compile(r"(fir_mxh_kernel|fir_mxi_kernel|fir_mx_kernel)I")
     seen = {n for n in names if n and two_wave.search(n)}
-    assert len(seen) >= 14, sorted(seen)
+    assert len(seen) >= 20, sorted(seen)
     uncovered = [(names[a], lines[a].strip()) for a, _, cov, _ in pairs
                  if not cov and names[a] and two_wave.search(names[a])]
-    assert not uncovered, f"uncovered packed-f32 pairs in two-wave MFMA kernels: {uncovered[:4]}"
+    assert not uncovered, f"uncovered packed-f32 pairs in MFMA FIR kernels: {uncovered[:4]}"
     covered = [names[a] for a, _, cov, _ in pairs if cov and names[a] and two_wave.search(names[a])]
     # fir_mxi's output combination (2^16 C2 + 2^8 C1 + C0) 2^-s: 14 pairs, each behind the
     # compiler's s_nop 0 (never seen to fail); fir_mxh: none

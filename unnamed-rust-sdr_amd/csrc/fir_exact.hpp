@@ -14,26 +14,38 @@ namespace sdrgpu {
 // (fir.rs:28-30, convolve.rs:13-15): acc = 0; acc += x[g - k] * h[k] for k = 0 .. K-1, the
 // num-complex product, no FMA, x[< 0] from the carried history.  Non-finite outputs are then
 // exactly the reference's.
-__device__ __forceinline__ float exact_prod(float x, float h) {
-#pragma clang fp contract(off)
-    return x * h;
+// The arithmetic is written as VOP2 instructions: plain C++ lets the compiler pair the re / im
+// halves into packed-f32 ops, and a packed product read by the next packed op without a wait
+// state went wrong in lanes 48-63 beside another wave's MFMAs (DESIGN.md 3.6,
+// profiles/r06_pkfault.txt).  The MFMA kernels that call these need that; the others lose
+// nothing that matters on a path only inf / NaN samples take.  IEEE-exact, no contraction.
+__device__ __forceinline__ float vop2_mul(float a, float b) {
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
+__device__ __forceinline__ float vop2_add(float a, float b) {
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vop2_sub(float a, float b) {
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float exact_prod(float x, float h) { return vop2_mul(x, h); }
 __device__ __forceinline__ c64 exact_prod(c64 x, float h) {
-#pragma clang fp contract(off)
-    return make_float2(x.x * h, x.y * h);
+    return make_float2(vop2_mul(x.x, h), vop2_mul(x.y, h));
 }
 __device__ __forceinline__ c64 exact_prod(c64 x, c64 h) {
-#pragma clang fp contract(off)
-    return make_float2(x.x * h.x - x.y * h.y, x.x * h.y + x.y * h.x);
+    return make_float2(vop2_sub(vop2_mul(x.x, h.x), vop2_mul(x.y, h.y)),
+                       vop2_add(vop2_mul(x.x, h.y), vop2_mul(x.y, h.x)));
 }
-__device__ __forceinline__ void exact_add(float& a, float b) {
-#pragma clang fp contract(off)
-    a += b;
-}
+__device__ __forceinline__ void exact_add(float& a, float b) { a = vop2_add(a, b); }
 __device__ __forceinline__ void exact_add(c64& a, c64 b) {
-#pragma clang fp contract(off)
-    a.x += b.x;
-    a.y += b.y;
+    a.x = vop2_add(a.x, b.x);
+    a.y = vop2_add(a.y, b.y);
 }
 constexpr int kExactBatch = 8;
 // P: FirParams, or a kernel's own parameter block with the same i0 / n_in / K / D / taps_pm / tpp
