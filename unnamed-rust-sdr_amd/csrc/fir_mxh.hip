@@ -534,7 +534,9 @@ void fir_mxh_kernel(MxhParams p) {
     static_assert(NG <= 8 && 2 * NG > 8, "one raw tile in flight");
     static_assert(NG > NH, "an even window's last NH groups come from keep[]");
     Cur cm, st, ld;
-    seek(cm, p.blocked ? (int)((long)blockIdx.x * p.units / gridDim.x) + wv : (int)wave);
+    const int first_unit = p.blocked ? (int)((long)blockIdx.x * p.units / gridDim.x) + wv : (int)wave;
+    int nf_tiles = 0;  // tiles whose window held inf / NaN (wave-uniform)
+    seek(cm, first_unit);
     if (cm.ok) {
         Raw nx[NG], hr[NH];
         load_hist(hr, cm);
@@ -663,7 +665,7 @@ void fir_mxh_kernel(MxhParams p) {
             const int so = -(s_cur + p.sh);
             const int tile = cm.tu + cm.t;
             if (!U8 && s_cur == kNonFinite) {
-                exact_tile<D, CS>(p, cm.ch, tile, sv, g);
+                ++nf_tiles;  // its outputs come from exact_tile after the main loop
             } else {
                 float2* __restrict__ out = p.out + cm.ch * p.ld_out;
                 // the tile's output base is scalar; the lanes' byte offsets inside it are fixed
@@ -708,6 +710,27 @@ void fir_mxh_kernel(MxhParams p) {
             body(std::integral_constant<int, 0>());
             if (!cm.ok) break;
             body(std::integral_constant<int, 1>());
+        }
+    }
+    if constexpr (!U8) {
+        // the tiles the loop skipped: walk the wave's tiles again and give every one whose
+        // window [j0 - H, j0 + TI) holds inf / NaN (exactly those whose scale was kNonFinite)
+        // the reference's sums -- out of the main loop, so its code leaves the loop's
+        // registers and schedule alone
+        if (nf_tiles > 0) {
+            Cur c;
+            seek(c, first_unit);
+            while (c.ok) {
+                const long j0 = tile_j0(c) - H;
+                bool bad = false;
+                for (int q = lane; q < H + TI; q += 64) {
+                    const float2 xv = fetch1(p.in + c.ch * p.ld_in, p.hist + c.ch * (long)(K - 1),
+                                             j0 + q, n_in, K);
+                    bad |= !(__builtin_isfinite(xv.x) && __builtin_isfinite(xv.y));
+                }
+                if (__builtin_amdgcn_ballot_w64(bad) != 0) exact_tile<D, CS>(p, c.ch, c.tu + c.t, sv, g);
+                adv(c);
+            }
         }
     }
 
