@@ -41,6 +41,6 @@ for name, sk, D, nch, n in shapes:
         else:
             f.process_dev(dx.ptr, n, dy.ptr, n_out)
         synchronize()
-        h = hashlib.sha1(dy.download(n_out * nch, np.uint8 if False else np.complex64).tobytes()).hexdigest()[:12]
+        h = hashlib.sha1(dy.download(n_out * nch, np.complex64).tobytes()).hexdigest()[:12]
         hashes[h] = hashes.get(h, 0) + 1
     print(f"{name:32s} kernel={f.last_kernel()} {REPS} launches, {len(hashes)} distinct outputs {hashes}", flush=True)

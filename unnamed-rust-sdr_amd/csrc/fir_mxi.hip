@@ -59,6 +59,20 @@ constexpr int kCs1 = 4;       // D = 1: four sets, so a tile is 1024 new samples
 constexpr int kCs2 = 2;       // D = 2: two sets
 constexpr int kRunTiles = 8;  // per-workgroup runs of 8 x 256 outputs (as the fp16 u8 launch)
 
+// (2^16 C2 + 2^8 C1 + C0) 2^-(S+7) as fmaf(C2, sc2, fmaf(C1, sc1, C0 sc0)), written as VOP3
+// v_mul_f32 / v_fma_f32: plain C++ lets the compiler pair the re and im combinations into
+// packed-f32 ops, and packed-f32 results went wrong beside another wave's MFMAs on the SIMD in
+// this library twice (profiles/r06_pkfault.txt) -- this kernel runs two waves
+// per SIMD.  Same roundings, same bytes.
+__device__ __forceinline__ float digits_f32(int c0, int c1, int c2, float sc0, float sc1, float sc2) {
+    const float a = (float)c0, b = (float)c1, d = (float)c2;
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(sc0));
+    asm("v_fma_f32 %0, %1, %2, %0" : "+v"(r) : "v"(b), "v"(sc1));
+    asm("v_fma_f32 %0, %1, %2, %0" : "+v"(r) : "v"(d), "v"(sc2));
+    return r;
+}
+
 template <int NC, int CS, int D>
 struct GeoI {
     static constexpr int HR = 64 * NC - 16 * D;   // history samples a tile's window needs
@@ -334,8 +348,8 @@ void fir_mxi_kernel(MxiParams p) {
                     float yr[4], yi[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        yr[q] = fmaf((float)acc[0][2][q], sc2, fmaf((float)acc[0][1][q], sc1, (float)acc[0][0][q] * sc0));
-                        yi[q] = fmaf((float)acc[1][2][q], sc2, fmaf((float)acc[1][1][q], sc1, (float)acc[1][0][q] * sc0));
+                        yr[q] = digits_f32(acc[0][0][q], acc[0][1][q], acc[0][2][q], sc0, sc1, sc2);
+                        yi[q] = digits_f32(acc[1][0][q], acc[1][1][q], acc[1][2][q], sc0, sc1, sc2);
                     }
                     if (p.vec_out && m0 + 256 <= p.n_out) {
                         // line-complete stores (fir_mxh.hip): lanes v and v^1 swap one 16-B half
