@@ -110,13 +110,34 @@ __global__ __launch_bounds__(kFftBlock) void fft_tile_kernel(TileArgs a) {
     // coalesced load: point p -> (frame p / M, sample p % M), all 16 loads in flight
     {
         float2 v[16];
-        gather_tile<16, kFftBlock>(a.src, M, f0, nf, kTile, [](int p) { return p / M; }, v);
+        gather_tile_ct<16, kFftBlock, M, kTile>(a.src, f0, nf, v);
 #pragma unroll
         for (int i = 0; i < 16; ++i) lds[fpad(t + kFftBlock * i)] = v[i];
     }
     __syncthreads();
     tile_fft<M, false>(lds, a.tw);
-    if (a.store_mode == 0 || a.store_mode == 3) {
+    if ((a.store_mode == 0 || a.store_mode == 3) && nf == fpt) {
+        // full tile: output (f, o) is element p = f M + o of the tile's contiguous output run,
+        // a 32-bit offset off one scalar base; every LDS read issued before the first store
+        const bool db = a.store_mode == 3;
+        char* base = reinterpret_cast<char*>(a.out) + f0 * M * (db ? 4 : 8);
+        float2 x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int p = t + kFftBlock * i, o = p % M;
+            x[i] = lds[fpad(o + M / 2 < M ? p + M / 2 : p + M / 2 - M)];
+        }
+        if (db) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                *reinterpret_cast<float*>(base + (unsigned)(t + kFftBlock * i) * 4u) = db_of(x[i], a.norm);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                *reinterpret_cast<float2*>(base + (unsigned)(t + kFftBlock * i) * 8u) =
+                    make_float2(x[i].x * a.norm, x[i].y * a.norm);
+        }
+    } else if (a.store_mode == 0 || a.store_mode == 3) {
         // collated store, output-ordered (coalesced): out[f][i] = X[(i + M/2) % M] * norm
         const int half = M / 2;
 #pragma unroll 4

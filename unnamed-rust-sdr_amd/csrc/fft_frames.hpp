@@ -121,6 +121,45 @@ __device__ __forceinline__ void gather_tile(const FrameSrc& s, long M, long f0, 
     }
 }
 
+// Gather for kernels whose frame size M and tile length L are compile-time constants (the
+// power-of-two tile kernel, the compile-time mixed-radix plans).  A full workgroup (all B frames present, every one inside
+// the input) reads point p = f N + n of its tile (N = M) at sample p + f (stride - N) of its first
+// frame: a 32-bit byte offset off a scalar base, with no per-point bounds selects and no
+// 64-bit address chain (the generic gather_tile spends ~12 VALU per point on those, and the
+// live spectrum is VALU-bound).  Same samples, so the transform's results are unchanged;
+// every other workgroup takes gather_tile.
+template <int PER, int BLK, int N, int L>
+__device__ __forceinline__ void gather_tile_ct(const FrameSrc& s, long f0, int nf, float2 (&v)[PER]) {
+    constexpr int B = L / N;
+    const FrameFast q = frame_fast(s, N, f0, nf);
+    const int t = threadIdx.x;
+    if (nf == B && (q.kind == 1 || q.kind == 3) && (B - 1) * q.stride + N < (1L << 28)) {
+        const int d = (int)(q.stride - N);
+        if (q.kind == 1) {
+            const char* base = reinterpret_cast<const char*>(q.c);
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int p = t + u * BLK, f = p / N;
+                const unsigned off = (unsigned)(p + f * d) * 8u;
+                v[u] = p < L ? *reinterpret_cast<const float2*>(base + off) : make_float2(0.f, 0.f);
+            }
+        } else {
+            const char* base = reinterpret_cast<const char*>(q.u);
+            unsigned short w[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int p = t + u * BLK, f = p / N;
+                const unsigned off = (unsigned)(p + f * d) * 2u;
+                w[u] = p < L ? *reinterpret_cast<const unsigned short*>(base + off) : (unsigned short)0x8080;
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u) v[u] = u8_sample(w[u]);
+        }
+        return;
+    }
+    gather_tile<PER, BLK>(s, N, f0, nf, L, [](int p) { return p / N; }, v);
+}
+
 // Store modes (bin k of frame f):
 //   0 collated fft: out[(k + M/2) mod M] = X[k] * norm (fft.rs:14-26)
 //   1 rfft: collated [M/2, M) = X[0, M - M/2) * norm (fft.rs:35)

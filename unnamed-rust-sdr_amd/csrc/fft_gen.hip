@@ -313,6 +313,8 @@ __device__ __forceinline__ void fixed_pass(float2* buf, const float2* __restrict
             const int s0 = f * N + j;
 #pragma unroll
             for (int r = 0; r < R; ++r) v[u][r] = buf[lp<TILE>(s0 + r * Q)];
+            // (the R - 1 powers read from the table instead: 1000 points 0.42 -> 0.55 ms, the
+            // loads' latency costs more than the product tree's VALU, profiles/r06_fftfixed.txt)
             if (NS > 1) twiddle_tree<R>(v[u], tw[k * STEP]);
             dft_any<R>(v[u], tw, N);
             dsto[u] = f * N + (j - k) * R + k;
@@ -335,44 +337,6 @@ __device__ __forceinline__ void fixed_engine(float2* buf, const float2* __restri
     if constexpr (sizeof...(REST) > 0) fixed_engine<BLK, TILE, N, B, NS * R, REST...>(buf, tw);
 }
 
-// The compile-time kernels' gather.  A full workgroup (all B frames present, every one inside
-// the input) reads point p = f N + n of its tile at sample p + f (stride - N) of its first
-// frame: a 32-bit byte offset off a scalar base, with no per-point bounds selects and no
-// 64-bit address chain (the generic gather_tile spends ~12 VALU per point on those, and the
-// live spectrum is VALU-bound).  Same samples, so the transform's results are unchanged;
-// every other workgroup takes gather_tile.
-template <int PER, int BLK, int N, int L>
-__device__ __forceinline__ void gather_fixed(const FrameSrc& s, long f0, int nf, float2 (&v)[PER]) {
-    constexpr int B = L / N;
-    const FrameFast q = frame_fast(s, N, f0, nf);
-    const int t = threadIdx.x;
-    if (nf == B && (q.kind == 1 || q.kind == 3) && (B - 1) * q.stride + N < (1L << 28)) {
-        const int d = (int)(q.stride - N);
-        if (q.kind == 1) {
-            const char* base = reinterpret_cast<const char*>(q.c);
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int p = t + u * BLK, f = p / N;
-                const unsigned off = (unsigned)(p + f * d) * 8u;
-                v[u] = p < L ? *reinterpret_cast<const float2*>(base + off) : make_float2(0.f, 0.f);
-            }
-        } else {
-            const char* base = reinterpret_cast<const char*>(q.u);
-            unsigned short w[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int p = t + u * BLK, f = p / N;
-                const unsigned off = (unsigned)(p + f * d) * 2u;
-                w[u] = p < L ? *reinterpret_cast<const unsigned short*>(base + off) : (unsigned short)0x8080;
-            }
-#pragma unroll
-            for (int u = 0; u < PER; ++u) v[u] = u8_sample(w[u]);
-        }
-        return;
-    }
-    gather_tile<PER, BLK>(s, N, f0, nf, L, [](int p) { return p / N; }, v);
-}
-
 template <int BLK, int TILE, int N, int... RS>
 __global__ __launch_bounds__(BLK) void gen_fixed_kernel(GenTileArgs a) {
     extern __shared__ float2 glds[];
@@ -383,7 +347,7 @@ __global__ __launch_bounds__(BLK) void gen_fixed_kernel(GenTileArgs a) {
     {
         constexpr int PER = TILE / BLK;
         float2 v[PER];
-        gather_fixed<PER, BLK, N, L>(a.src, f0, nf, v);
+        gather_tile_ct<PER, BLK, N, L>(a.src, f0, nf, v);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int p = threadIdx.x + u * BLK;
