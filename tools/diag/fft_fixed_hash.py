@@ -44,3 +44,8 @@ for n, frames in ((1000, 4097), (14400, 33), (1024, 1031), (4096, 77), (16, 9999
     for out in ("complex", "db"):
         y = sdrgpu.fft.FftPlan(n, output=out).exec(x.reshape(frames, n))
         print(f"fft n={n} frames={frames} out={out}: {hashlib.sha256(y.tobytes()).hexdigest()[:16]}", flush=True)
+for n, frames in ((14400, 37), (14400, 4096)):
+    x = rng.standard_normal(n * frames).astype(np.float32)
+    for out in ("complex", "db"):
+        y = sdrgpu.fft.FftPlan(n, output=out).exec_real(x.reshape(frames, n))
+        print(f"rfft n={n} frames={frames} out={out}: {hashlib.sha256(y.tobytes()).hexdigest()[:16]}", flush=True)

@@ -42,3 +42,24 @@ for n, hop in ((1000, 500), (1024, 512), (4096, 2048)):
         t = float(np.median(ms))
         print(f"n={n} hop={hop} in={'u8' if kind == _lib.CU8 else 'c64'} out={out:7s} {t:.4f} ms  "
               f"{byt / t / 1e9:.0f} GB/s = {byt / t / 8e9:.3f} of 8 TB/s", flush=True)
+# examples/fft.rs: 14,400-point rfft over 4096 real frames (packed half-length kernel)
+for out in ("complex", "db"):
+    p = sdrgpu.fft.FftPlan(14400, output=out)
+    xr = rng.standard_normal(14400 * 4096).astype(np.float32)
+    dx = DeviceBuffer(xr.nbytes)
+    dx.upload(xr)
+    ob = 4 if out == "db" else 8
+    dy = DeviceBuffer(4096 * 7200 * ob)
+    st = p.stream()
+    ms = []
+    for it in range(13):
+        a, b = Event(), Event()
+        a.record(st)
+        p.exec_real_dev(dx.ptr, dy.ptr, 4096)
+        b.record(st)
+        b.synchronize()
+        if it >= 3:
+            ms.append(a.elapsed_ms(b))
+    t = float(np.median(ms))
+    byt = xr.nbytes + 4096 * 7200 * ob
+    print(f"n=14400 rfft x4096 out={out:7s} {t:.4f} ms  {byt / t / 8e9:.3f} of 8 TB/s", flush=True)

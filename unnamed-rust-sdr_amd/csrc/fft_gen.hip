@@ -420,7 +420,7 @@ __global__ __launch_bounds__(BLK) void gen_rfft_half_kernel(GenTileArgs a, const
     {
         constexpr int PER = TILE / BLK;
         float2 v[PER];
-        gather_tile<PER, BLK>(a.src, NH, f0, nf, L, [](int p) { return p / NH; }, v);
+        gather_tile_ct<PER, BLK, NH, L>(a.src, f0, nf, v);
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int p = threadIdx.x + u * BLK;
@@ -429,16 +429,24 @@ __global__ __launch_bounds__(BLK) void gen_rfft_half_kernel(GenTileArgs a, const
     }
     __syncthreads();
     fixed_engine<BLK, TILE, NH, B, 1, RS...>(b0, twh);
-    for (int p = threadIdx.x; p < nf * NH; p += BLK) {
-        const int f = p / NH, k = p - f * NH;
-        const float2 z = b0[lp<TILE>(p)];
-        const float2 m = b0[lp<TILE>(f * NH + (k ? NH - k : 0))];
-        const float ex = 0.5f * (z.x + m.x), ey = 0.5f * (z.y - m.y);
-        const float ox = 0.5f * (z.y + m.y), oy = -0.5f * (z.x - m.x);
-        const float2 w = a.tw[k];  // W_N^k, N = 2 NH
-        const float2 x = make_float2(ex + (w.x * ox - w.y * oy), ey + (w.x * oy + w.y * ox));
-        if (a.store_mode == 1) a.out[(f0 + f) * NH + k] = make_float2(x.x * a.norm, x.y * a.norm);
-        else reinterpret_cast<float*>(a.out)[(f0 + f) * NH + k] = db_of(x, a.norm);
+    // bin (f, k) is element p = f NH + k of the workgroup's contiguous output run: a 32-bit
+    // offset off one scalar base
+    const bool db = a.store_mode != 1;
+    char* base = reinterpret_cast<char*>(a.out) + f0 * NH * (db ? 4 : 8);
+#pragma unroll 2  // (fully unrolled: 70 VGPRs, one workgroup per CU fewer)
+    for (int u = 0; u < (L + BLK - 1) / BLK; ++u) {
+        const int p = threadIdx.x + u * BLK;
+        if (p < L && p < nf * NH) {
+            const int f = p / NH, k = p - f * NH;
+            const float2 z = b0[lp<TILE>(p)];
+            const float2 m = b0[lp<TILE>(f * NH + (k ? NH - k : 0))];
+            const float ex = 0.5f * (z.x + m.x), ey = 0.5f * (z.y - m.y);
+            const float ox = 0.5f * (z.y + m.y), oy = -0.5f * (z.x - m.x);
+            const float2 w = a.tw[k];  // W_N^k, N = 2 NH
+            const float2 x = make_float2(ex + (w.x * ox - w.y * oy), ey + (w.x * oy + w.y * ox));
+            if (!db) *reinterpret_cast<float2*>(base + (unsigned)p * 8u) = make_float2(x.x * a.norm, x.y * a.norm);
+            else *reinterpret_cast<float*>(base + (unsigned)p * 4u) = db_of(x, a.norm);
+        }
     }
 }
 
