@@ -13,7 +13,7 @@ from sdrgpu.device import DeviceBuffer, synchronize  # noqa: E402
 n_in = 1 << 26
 rng = np.random.default_rng(3)
 x = (rng.standard_normal(1 << 22) + 1j * rng.standard_normal(1 << 22)).astype(np.complex64)
-s = sdrgpu.fft.Stft(1000, 500, output=os.environ.get("OUT", "db"))
+s = sdrgpu.fft.Stft(1000, 500, output=os.environ.get("LIVE_OUT", "db"))
 dx = DeviceBuffer(n_in * 8)
 for off in range(0, n_in * 8, x.nbytes):
     dx.upload(x, offset_bytes=off)
