@@ -16,7 +16,7 @@ n_in = 1 << 26
 rng = np.random.default_rng(3)
 x = (rng.standard_normal(1 << 22) + 1j * rng.standard_normal(1 << 22)).astype(np.complex64)
 xu = rng.integers(0, 256, size=2 << 22, dtype=np.uint8)
-for n, hop in ((1000, 500), (1024, 512), (4096, 2048)):
+for n, hop in ((1000, 500), (1024, 512), (4096, 2048), (1200, 600), (3000, 1500), (6000, 3000)):
     for out, kind in (("complex", _lib.C64), ("db", _lib.C64), ("db", _lib.CU8)):
         s = sdrgpu.fft.Stft(n, hop, input_kind=kind, output=out)
         eb = 2 if kind == _lib.CU8 else 8

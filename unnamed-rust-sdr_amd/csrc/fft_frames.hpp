@@ -83,6 +83,32 @@ __device__ __forceinline__ void gather_tile(const FrameSrc& s, long M, long f0, 
                                             const Div& div, float2 (&v)[PER]) {
     const FrameFast q = frame_fast(s, M, f0, nf);
     const int t = threadIdx.x;
+    if ((q.kind == 1 || q.kind == 3) && nf * M == L && (nf - 1) * q.stride + M < (1L << 28)) {
+        // every frame of the tile present and inside the input: point p = f M + n sits at
+        // sample p + f (stride - M) of the first frame, a 32-bit byte offset off a scalar base
+        const int d = (int)(q.stride - M);
+        if (q.kind == 1) {
+            const char* base = reinterpret_cast<const char*>(q.c);
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int p = t + u * BLK;
+                const unsigned off = (unsigned)(p + div(p) * d) * 8u;
+                v[u] = p < L ? *reinterpret_cast<const float2*>(base + off) : make_float2(0.f, 0.f);
+            }
+        } else {
+            const char* base = reinterpret_cast<const char*>(q.u);
+            unsigned short w[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int p = t + u * BLK;
+                const unsigned off = (unsigned)(p + div(p) * d) * 2u;
+                w[u] = p < L ? *reinterpret_cast<const unsigned short*>(base + off) : (unsigned short)0x8080;
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u) v[u] = u8_sample(w[u]);
+        }
+        return;
+    }
     if (q.kind == 1) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {

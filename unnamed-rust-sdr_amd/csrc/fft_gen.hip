@@ -271,16 +271,29 @@ __global__ __launch_bounds__(BLK) void gen_tile_kernel(GenTileArgs a) {
     gen_engine<BLK, TILE>(b0, N, B, a.rl, a.tw);
     const float2* X = b0;
     if (a.store_mode == 0 || a.store_mode == 3) {
-        // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o
+        // output-ordered: out[o] = X[(o - N/2) mod N] * norm, consecutive lanes -> consecutive o;
+        // the dB store writes output (f, o) as element p = f N + o of the workgroup's contiguous
+        // output run, a 32-bit offset off one scalar base (the c64 store the same way measured
+        // 1-2 % slower at 1200 / 6000 points, faster at 3000: not taken, profiles/r06_fftfixed.txt)
         const int sh = N - N / 2;
+        const bool db = a.store_mode == 3;
+        char* base = reinterpret_cast<char*>(a.out) + f0 * N * 4;
+        if (db) {
 #pragma unroll 4
-        for (int p = threadIdx.x; p < nf * N; p += BLK) {
-            const int f = a.rl.dn.div(p), o = p - f * N;
-            int k = o + sh;
-            if (k >= N) k -= N;
-            const float2 x = X[lp<TILE>(f * N + k)];
-            if (a.store_mode == 0) a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
-            else reinterpret_cast<float*>(a.out)[(f0 + f) * N + o] = db_of(x, a.norm);
+            for (int p = threadIdx.x; p < nf * N; p += BLK) {
+                const int f = a.rl.dn.div(p), o = p - f * N;
+                const float2 x = X[lp<TILE>(o + sh < N ? p + sh : p + sh - N)];
+                *reinterpret_cast<float*>(base + (unsigned)p * 4u) = db_of(x, a.norm);
+            }
+        } else {
+#pragma unroll 4
+            for (int p = threadIdx.x; p < nf * N; p += BLK) {
+                const int f = a.rl.dn.div(p), o = p - f * N;
+                int k = o + sh;
+                if (k >= N) k -= N;
+                const float2 x = X[lp<TILE>(f * N + k)];
+                a.out[(f0 + f) * N + o] = make_float2(x.x * a.norm, x.y * a.norm);
+            }
         }
     } else {
         for (int p = threadIdx.x; p < nf * N; p += BLK) {
