@@ -437,3 +437,36 @@ def test_stft_u8_input(sdr, oracle):
         assert y.shape == ref.shape
         for j in range(ref.shape[0]):
             assert_parity(y[j], ref[j], what=f"u8 stft n={n} frame {j}")
+
+
+@pytest.mark.parametrize("n,hop", [(1000, 500), (1000, 1300), (1024, 512), (4096, 1000), (1200, 600),
+                                   (6000, 3000), (14400, 7200)])
+@pytest.mark.parametrize("u8", [False, True])
+def test_stft_full_workgroup_gather(sdr, oracle, n, hop, u8):
+    """Streams long enough that most workgroups take the full-workgroup 32-bit gather / store
+    (fft_frames.hpp gather_tile_ct / gather_tile fast path), the first ones the history path and
+    the last a ragged tile, in two blocks (the second starting from carried history); c64 and
+    dB outputs against the oracle.  Compile-time plans (1000, 14400), power-of-two tiles (1024,
+    4096), the generic mixed-radix tile (1200, 6000)."""
+    from sdrgpu import _lib
+    rng = np.random.default_rng(n + hop + u8)
+    n_in = hop * 37 + 123
+    if u8:
+        iq = rng.integers(0, 256, 2 * n_in, dtype=np.uint8)
+        x, cut, kind = oracle.u8_to_c64(iq), 2 * (hop * 9 + 17), _lib.CU8
+        parts = (iq[:cut], iq[cut:])
+    else:
+        x = cplx(rng, n_in)
+        cut, kind = hop * 9 + 17, _lib.C64
+        parts = (x[:cut], x[cut:])
+    ref = oracle.stft(x, n, hop, nthreads=8)
+    s = sdr.fft.Stft(n, hop, input_kind=kind)
+    y = np.concatenate([s.process(p) for p in parts])
+    assert y.shape == ref.shape
+    for j in range(ref.shape[0]):
+        assert_parity(y[j], ref[j], what=f"stft n={n} hop={hop} u8={u8} frame {j}")
+    s = sdr.fft.Stft(n, hop, input_kind=kind, output="db")
+    yd = np.concatenate([s.process(p) for p in parts])
+    assert yd.shape == ref.shape and yd.dtype == np.float32
+    for j in range(0, ref.shape[0], 5):
+        _check_db(yd[j], ref[j], f"stft db n={n} hop={hop} u8={u8} frame {j}")
